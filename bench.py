@@ -1,0 +1,241 @@
+#!/usr/bin/env python3
+"""bench.py -- value-block CRC throughput on MI355X (BASELINE.json metric).
+
+One "step" = one pass of priskv_crc32 (server/crc.c:90-109) over every value
+block of this GPU's shard, device-resident (inputs already in HBM when the
+timed region starts), through the library's C ABI
+(priskv_crc32_blocks_dev, include/priskv_crc_gpu.h).
+
+Default workload (BASELINE.json configs[1]): 1 Mi x 4 KiB blocks = 4 GiB per
+GPU.  For N > 1 (launched by torch.distributed.run) each rank owns its own
+4 GiB shard -- the next 1 Mi blocks of one global region -- and checksums it
+with no data-path collective ("weak" scaling); the barrier and the max-over-
+ranks reduction are the benchmark contract, not part of the path.
+
+Prints ONE JSON line on rank 0.  Extra keys:
+  roofline      dominant kernel (crc_rows_kernel) vs the HBM roof: algorithmic
+                bytes per launch / average launch time (HIP events on the launch
+                stream); traffic = PMC-measured HBM bytes per launch for this
+                workload when profiles/ holds a matching measurement, else null
+  cpu_baseline  rank 0 at N=1: the reference's own server/crc.c (compiled -O2
+                into oracle/_ref) timed single-threaded on a bounded sample of
+                the same blocks, which also serves as a bit-exact spot check
+  parity        result of comparing the GPU CRCs with that CPU sample
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "GiB/s CRC over device-resident value blocks at 1/2/4/8 MI355X"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
+SEED = 0x5EED5EED
+
+CONFIGS = {
+    # name: (block_size, nblocks per GPU, description)
+    "default": (4096, 1 << 20, "1Mi x 4KiB value blocks per GPU, device-resident (4 GiB/GPU)"),
+    "sweep64k": (65536, 1 << 16, "64Ki x 64KiB value blocks per GPU, device-resident (4 GiB/GPU)"),
+    "sweep1m": (1 << 20, 1 << 12, "4Ki x 1MiB value blocks per GPU, device-resident (4 GiB/GPU)"),
+    "tib": (65536, 1 << 21, "2Mi x 64KiB value blocks per GPU (128 GiB/GPU; 1 TiB at 8 GPUs)"),
+}
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--config", default="default", choices=sorted(CONFIGS) + ["streamed"])
+    p.add_argument("--block-size", type=int, default=None)
+    p.add_argument("--nblocks", type=int, default=None)
+    p.add_argument("--cpu-sample-bytes", type=int, default=3 << 30,
+                   help="bytes of the shard the CPU baseline hashes (about 10 s at -O2)")
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    return p.parse_args()
+
+
+def load_traffic(cfg_name: str, block_size: int, nblocks: int):
+    """HBM bytes per launch from a committed rocprofv3 PMC summary, if one matches."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        e = d.get(f"{block_size}x{nblocks}")
+        return None if e is None else float(e["hbm_bytes_per_launch"])
+    except (OSError, ValueError, KeyError):
+        return None
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and rank == 0:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    from priskv_amd import CrcContext, as_u32
+
+    if args.config == "streamed":
+        return streamed(args, torch, rank, world)
+
+    bs, nb, desc = CONFIGS[args.config]
+    if args.block_size:
+        bs = args.block_size
+    if args.nblocks:
+        nb = args.nblocks
+    ctx = CrcContext(local)
+    region = torch.empty(bs * nb, dtype=torch.uint8, device=dev)
+    # this rank's shard = blocks [rank*nb, (rank+1)*nb) of one global region
+    ctx.fill_splitmix(region, SEED, word_offset=rank * (bs * nb // 8))
+    out = torch.empty(nb, dtype=torch.int32, device=dev)
+    stream = torch.cuda.current_stream()
+    torch.cuda.synchronize()
+
+    for _ in range(args.warmup):
+        ctx.blocks_dev(region, bs, out=out, stream=stream)
+    torch.cuda.synchronize()
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev1 = torch.cuda.Event(enable_timing=True)
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for _ in range(args.steps):
+        ctx.blocks_dev(region, bs, out=out, stream=stream)
+    ev1.record(stream)
+    torch.cuda.synchronize()
+    barrier()
+    t1 = time.perf_counter()
+    elapsed = t1 - t0
+    kernel_ms = ev0.elapsed_time(ev1) / args.steps  # launches back-to-back on `stream`
+
+    el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    elapsed_max = float(el.item())
+
+    total_bytes = bs * nb * world
+    value = total_bytes * args.steps / elapsed_max / 2**30
+    alg_bytes = nb * (bs + 4)  # block read + 4-byte CRC written
+    achieved = alg_bytes / (kernel_ms * 1e-3) / 1e9
+    traffic = load_traffic(args.config, bs, nb)
+    path = ctx_path(bs, region)
+
+    result = {
+        "metric": METRIC,
+        "value": round(value, 2),
+        "unit": "GiB/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed_max / args.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic (splitmix64 pattern filled on device)",
+        "config": {"workload": desc, "block_size": bs, "nblocks_per_gpu": nb,
+                   "bytes_per_gpu": bs * nb, "parallelism": f"shard{world} (contiguous block ranges, no collective)",
+                   "kernel": path},
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBS, 4),
+                     "traffic": traffic, "kernel_ms": round(kernel_ms, 4),
+                     "alg_bytes_per_launch": alg_bytes},
+    }
+
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        import _oracle as O
+        nsamp = max(1, min(nb, args.cpu_sample_bytes // bs))
+        host = region[: nsamp * bs].cpu().numpy()
+        secs, cpu_crc, kind, label = O.time_cpu_baseline(host, bs)
+        gpu_crc = as_u32(out[:nsamp])
+        ok = bool(np.array_equal(cpu_crc, gpu_crc))
+        result["cpu_baseline"] = {"value": round(nsamp * bs / secs / 2**30, 4), "unit": "GiB/s", "cores": 1,
+                                  "kind": kind,
+                                  "sample": f"first {nsamp} x {bs} B blocks ({nsamp * bs / 2**30:.2f} GiB) of the "
+                                            f"same shard, 1 thread, {label}; {secs:.1f} s",
+                                  "cpu": cpu_model()}
+        result["parity"] = {"checked_blocks": nsamp, "bit_exact": ok}
+        if not ok:
+            bad = np.nonzero(cpu_crc != gpu_crc)[0]
+            result["parity"]["first_mismatch"] = int(bad[0])
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def ctx_path(bs, region):
+    from priskv_amd import blocks_path
+    p = blocks_path(region.data_ptr(), 1, bs)
+    if p == "rows":
+        r = bs // 1024
+        return f"crc_rows_kernel<{4 if r % 4 == 0 else (2 if r % 2 == 0 else 1)}>"
+    return f"crc_{p}_kernel"
+
+
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for ln in f:
+                if ln.startswith("model name"):
+                    return ln.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def streamed(args, torch, rank, world):
+    """BASELINE config 5: 4 KiB blocks from pinned host memory, end to end."""
+    from priskv_amd import CrcContext, host_register, host_unregister
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import _oracle as O
+    bs = args.block_size or 4096
+    nb = args.nblocks or (1 << 20)
+    ctx = CrcContext(int(os.environ.get("LOCAL_RANK", "0")))
+    host = O.fill_splitmix(bs * nb, SEED, rank * (bs * nb // 8))
+    res = {}
+    for mode in ("pinned", "pageable"):
+        if mode == "pinned":
+            host_register(host)
+        out = ctx.blocks_host(host, bs)  # warm (allocates staging)
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            out = ctx.blocks_host(host, bs)
+        dt = (time.perf_counter() - t0) / args.steps
+        if mode == "pinned":
+            host_unregister(host)
+        res[mode] = round(bs * nb / dt / 2**30, 2)
+    samp = min(nb, 65536)
+    ok = bool(np.array_equal(out[:samp], O.crc32_blocks(host[: samp * bs], bs, nthreads=8)))
+    print(json.dumps({"metric": "GiB/s CRC of host-resident value blocks (PCIe-inclusive, streamed)",
+                      "value": res["pinned"], "unit": "GiB/s", "n_gpus": 1, "steps": args.steps,
+                      "pageable_GiBs": res["pageable"], "config": {"workload": f"{nb} x {bs} B host blocks",
+                                                                   "block_size": bs},
+                      "parity": {"checked_blocks": samp, "bit_exact": ok}}), flush=True)
+
+
+if __name__ == "__main__":
+    main()

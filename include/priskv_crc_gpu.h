@@ -1,0 +1,110 @@
+/*
+ * priskv_crc_gpu.h -- batched value-block CRC on MI355X (gfx950), C ABI.
+ *
+ * Every checksum computed here is bit-exact with PrisKV's priskv_crc32
+ * (server/crc.c:90-109: reflected polynomial 0xEDB88320, init 0, no final
+ * xor) applied to each value block on its own.  The reference has no batched
+ * or value-block entry point: priskv_crc32 (server/crc.h:37) is its only CRC
+ * interface, and these symbols are the new batched form SURVEY.md §8(b)
+ * prescribes, declared in a separate header so crc.h and its callers
+ * (server/kv.c:314,408, server/rdma.c:764) stay byte-for-byte unchanged.
+ *
+ * Data layout (the reference's value region, server/memory.h:87-91,
+ * server/memory.c:496-508, server/buddy.c:78,165): block i of a batch is the
+ * block_size bytes at base + i * block_size.
+ *
+ * Conventions (the reference's fallible-API style, e.g. server/memory.c:203-210):
+ *   return 0 on success or a negative errno:
+ *     -EINVAL  bad arguments (NULL pointers with n > 0, block_size 0, ...)
+ *     -ENODEV  no usable GPU / the device index does not exist
+ *     -ENOMEM  device or pinned-host allocation failed
+ *     -EIO     a HIP runtime call failed
+ *   Nothing here aborts the process, and there is no CPU fallback: a batch
+ *   either runs on the GPU or the call returns an error.
+ *
+ * Threading: a context is immutable after creation except for the staging
+ * buffers of the host-streamed path, which a per-context mutex serialises.
+ * The *_dev entry points are asynchronous on the caller's stream and may be
+ * called concurrently from any number of threads on one context.
+ *
+ * Streams are passed as `void *` holding a hipStream_t (NULL = the legacy
+ * default stream), so this header does not require the HIP headers.
+ */
+#ifndef PRISKV_CRC_GPU_H
+#define PRISKV_CRC_GPU_H
+
+#include <stdint.h>
+
+#if defined(__cplusplus)
+extern "C"
+{
+#endif
+
+typedef struct priskv_crc_ctx priskv_crc_ctx;
+
+/* Create a context on HIP device `device`: uploads the CRC tables (64 KiB
+ * LDS image + fold/shift matrices) and sizes the persistent grid from the
+ * device's CU count.  *out is set only on success. */
+int priskv_crc_ctx_create(int device, priskv_crc_ctx **out);
+void priskv_crc_ctx_destroy(priskv_crc_ctx *ctx);
+int priskv_crc_ctx_device(const priskv_crc_ctx *ctx);
+
+/* Device-resident batch: d_base -> nblocks * block_size bytes of device
+ * memory; d_out -> uint32_t[nblocks] of device memory.  d_out[i] =
+ * priskv_crc32(d_base + i*block_size, block_size).  Asynchronous on `stream`.
+ * Any block_size >= 1 and any d_base alignment are accepted; the fast path
+ * needs d_base 16-byte aligned and block_size a multiple of 1 KiB (or a power
+ * of two in [16, 512]) -- the reference's value blocks (4 KiB-aligned base,
+ * power-of-two size, server/memory.c:221,413-417) always qualify. */
+int priskv_crc32_blocks_dev(const priskv_crc_ctx *ctx, const void *d_base, uint64_t nblocks,
+                            uint32_t block_size, uint32_t *d_out, void *stream);
+
+/* Device-resident per-value extents: d_out[i] = priskv_crc32(d_base +
+ * d_offsets[i], d_lengths[i]) -- a value of valuelen bytes starting at
+ * value_off (priskv_key, server/memory.h:50-51).  d_offsets / d_lengths /
+ * d_out are device arrays of n entries.  Asynchronous on `stream`. */
+int priskv_crc32_ranges_dev(const priskv_crc_ctx *ctx, const void *d_base,
+                            const uint64_t *d_offsets, const uint32_t *d_lengths, uint64_t n,
+                            uint32_t *d_out, void *stream);
+
+/* Host-resident batch (the RDMA-registered value buffer / the memfile
+ * mapping): streams the blocks over PCIe in chunks on several HIP streams,
+ * overlapping H2D copies, kernels and the small D2H of results; synchronous.
+ * h_out is a host array of nblocks entries.  Pinned (hipHostMalloc) or
+ * registered (priskv_crc_host_register) input goes straight to the DMA
+ * engines; pageable input is bounced through the context's pinned staging. */
+int priskv_crc32_blocks_host(priskv_crc_ctx *ctx, const void *h_base, uint64_t nblocks,
+                             uint32_t block_size, uint32_t *h_out);
+
+/* Page-lock an existing host range (e.g. the mmap'd memfile value region,
+ * server/memory.c:351-457) for direct DMA, and undo it. */
+int priskv_crc_host_register(void *h_base, uint64_t len);
+int priskv_crc_host_unregister(void *h_base);
+
+/* GF(2) helpers (host, no GPU needed).  The reference CRC is linear with no
+ * affine term (init 0, xorout 0), so
+ *   priskv_crc32(A || B) == priskv_crc32_combine(crc(A), crc(B), |B|)
+ *   priskv_crc32_shift(c, n) == state c advanced over n zero bytes.      */
+uint32_t priskv_crc32_shift(uint32_t crc, uint64_t nbytes);
+uint32_t priskv_crc32_combine(uint32_t crc_a, uint32_t crc_b, uint64_t len_b);
+
+/* Deterministic test pattern on the device (benchmarks and parity tests):
+ * 64-bit little-endian word i of the region = splitmix64 output
+ * mix64(seed + (word_offset + i + 1) * 0x9E3779B97F4A7C15).  Asynchronous. */
+int priskv_crc_fill_splitmix_dev(const priskv_crc_ctx *ctx, void *d_dst, uint64_t nbytes,
+                                 uint64_t seed, uint64_t word_offset, void *stream);
+
+/* Which kernel a (d_base, block_size) batch dispatches to: 1 = rows (block
+ * a multiple of 1 KiB, one wave per block), 2 = rows, cooperative (blocks
+ * > 64 KiB: the waves of one workgroup split a block), 3 = sub-KiB
+ * power-of-two blocks, 4 = generic (any size / alignment).  For tests and
+ * benchmarks; -EINVAL for invalid arguments. */
+int priskv_crc32_blocks_path(const void *d_base, uint64_t nblocks, uint32_t block_size);
+
+const char *priskv_crc_version(void);
+
+#if defined(__cplusplus)
+}
+#endif
+
+#endif /* PRISKV_CRC_GPU_H */

@@ -1,0 +1,205 @@
+"""Python mirror of the value-block CRC C ABI (include/crc.h, include/priskv_crc_gpu.h).
+
+PrisKV's own interface for this path is the C function
+``uint32_t priskv_crc32(uint8_t *buf, uint32_t len)`` (server/crc.h:37,
+server/crc.c:90-109).  This module binds the in-tree ``libpriskv_crc.so``
+with ctypes -- exactly the binding a PrisKV maintainer would write (see
+INTEGRATION.md) -- and adds torch-tensor conveniences for tests and the
+benchmark.  torch is plumbing here (device memory, streams); every checksum
+is computed by the library's HIP kernels (or, for ``priskv_crc32`` itself,
+by its host C code).
+
+Errors follow the reference's 0 / -errno convention at the C boundary and
+surface here as ``OSError(errno, ...)``.  There is no CPU fallback for the
+batched calls: if the library or the GPU is missing they raise.
+"""
+from __future__ import annotations
+
+import ctypes
+import errno as _errno
+import os
+from typing import Optional
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libpriskv_crc.so")
+
+PATH_ROWS, PATH_ROWS_COOP, PATH_SMALL, PATH_GENERIC = 1, 2, 3, 4
+PATH_NAMES = {PATH_ROWS: "rows", PATH_ROWS_COOP: "rows_coop", PATH_SMALL: "small",
+              PATH_GENERIC: "generic"}
+
+_lib: Optional[ctypes.CDLL] = None
+
+# (name, restype, argtypes) for every symbol the two headers declare
+_C = ctypes
+SIGNATURES = [
+    ("priskv_crc32", _C.c_uint32, [_C.c_void_p, _C.c_uint32]),
+    ("priskv_crc_ctx_create", _C.c_int, [_C.c_int, _C.POINTER(_C.c_void_p)]),
+    ("priskv_crc_ctx_destroy", None, [_C.c_void_p]),
+    ("priskv_crc_ctx_device", _C.c_int, [_C.c_void_p]),
+    ("priskv_crc32_blocks_dev", _C.c_int,
+     [_C.c_void_p, _C.c_void_p, _C.c_uint64, _C.c_uint32, _C.c_void_p, _C.c_void_p]),
+    ("priskv_crc32_ranges_dev", _C.c_int,
+     [_C.c_void_p, _C.c_void_p, _C.c_void_p, _C.c_void_p, _C.c_uint64, _C.c_void_p, _C.c_void_p]),
+    ("priskv_crc32_blocks_host", _C.c_int,
+     [_C.c_void_p, _C.c_void_p, _C.c_uint64, _C.c_uint32, _C.c_void_p]),
+    ("priskv_crc_host_register", _C.c_int, [_C.c_void_p, _C.c_uint64]),
+    ("priskv_crc_host_unregister", _C.c_int, [_C.c_void_p]),
+    ("priskv_crc32_shift", _C.c_uint32, [_C.c_uint32, _C.c_uint64]),
+    ("priskv_crc32_combine", _C.c_uint32, [_C.c_uint32, _C.c_uint32, _C.c_uint64]),
+    ("priskv_crc_fill_splitmix_dev", _C.c_int,
+     [_C.c_void_p, _C.c_void_p, _C.c_uint64, _C.c_uint64, _C.c_uint64, _C.c_void_p]),
+    ("priskv_crc32_blocks_path", _C.c_int, [_C.c_void_p, _C.c_uint64, _C.c_uint32]),
+    ("priskv_crc_version", _C.c_char_p, []),
+]
+
+
+def lib() -> ctypes.CDLL:
+    """Load libpriskv_crc.so (raises if it has not been built)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(f"{LIB_PATH} not built: run `python -c 'import __graft_entry__ as g; "
+                              f"g.build()'` or `make -C priskv_amd/csrc`")
+        L = ctypes.CDLL(LIB_PATH)
+        for name, res, args in SIGNATURES:
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _lib = L
+    return _lib
+
+
+def _check(rc: int, what: str) -> None:
+    if rc != 0:
+        e = -rc
+        raise OSError(e, f"{what}: {_errno.errorcode.get(e, e)} ({os.strerror(e)})")
+
+
+# ---------------------------------------------------------------- host-side ABI
+def priskv_crc32(buf) -> int:
+    """server/crc.h:37 -- the drop-in host symbol (keys; synchronous, CPU)."""
+    a = np.frombuffer(memoryview(buf), dtype=np.uint8) if not isinstance(buf, np.ndarray) else buf
+    a = np.ascontiguousarray(a).view(np.uint8)
+    if a.size >= 2**32:
+        raise ValueError("priskv_crc32 takes a uint32_t length (server/crc.h:37)")
+    return int(lib().priskv_crc32(a.ctypes.data if a.size else None, a.size))
+
+
+def crc32_shift(crc: int, nbytes: int) -> int:
+    return int(lib().priskv_crc32_shift(crc & 0xFFFFFFFF, nbytes))
+
+
+def crc32_combine(crc_a: int, crc_b: int, len_b: int) -> int:
+    return int(lib().priskv_crc32_combine(crc_a & 0xFFFFFFFF, crc_b & 0xFFFFFFFF, len_b))
+
+
+def blocks_path(ptr: int, nblocks: int, block_size: int) -> str:
+    rc = lib().priskv_crc32_blocks_path(ptr, nblocks, block_size)
+    _check(rc if rc < 0 else 0, "priskv_crc32_blocks_path")
+    return PATH_NAMES[rc]
+
+
+def version() -> str:
+    return lib().priskv_crc_version().decode()
+
+
+def host_register(arr: np.ndarray) -> None:
+    _check(lib().priskv_crc_host_register(arr.ctypes.data, arr.nbytes), "priskv_crc_host_register")
+
+
+def host_unregister(arr: np.ndarray) -> None:
+    _check(lib().priskv_crc_host_unregister(arr.ctypes.data), "priskv_crc_host_unregister")
+
+
+# ---------------------------------------------------------------- context
+def _stream_ptr(stream) -> Optional[int]:
+    if stream is None:
+        import torch
+        return torch.cuda.current_stream().cuda_stream
+    if isinstance(stream, int):
+        return stream
+    return stream.cuda_stream
+
+
+class CrcContext:
+    """One libpriskv_crc context (device tables + streamed-path staging)."""
+
+    def __init__(self, device: int = 0):
+        self._h = ctypes.c_void_p()
+        _check(lib().priskv_crc_ctx_create(device, ctypes.byref(self._h)), "priskv_crc_ctx_create")
+        self.device = device
+
+    def close(self) -> None:
+        if self._h:
+            lib().priskv_crc_ctx_destroy(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    @property
+    def handle(self) -> ctypes.c_void_p:
+        return self._h
+
+    # ---- device-resident
+    def blocks_dev(self, region, block_size: int, out=None, stream=None, nblocks: Optional[int] = None):
+        """d_out[i] = priskv_crc32(region + i*block_size, block_size); returns an int32 cuda
+        tensor holding the uint32 bit patterns (asynchronous on `stream`)."""
+        import torch
+        if not region.is_cuda:
+            raise ValueError("region must be a device tensor (use blocks_host for host memory)")
+        nbytes = region.numel() * region.element_size()
+        n = nbytes // block_size if nblocks is None else nblocks
+        if n * block_size > nbytes:
+            raise ValueError("nblocks * block_size exceeds the region")
+        if out is None:
+            out = torch.empty(n, dtype=torch.int32, device=region.device)
+        if out.numel() < n or out.element_size() != 4 or not out.is_contiguous():
+            raise ValueError("out must be a contiguous 4-byte tensor of >= nblocks entries")
+        _check(lib().priskv_crc32_blocks_dev(self._h, region.data_ptr(), n, block_size, out.data_ptr(),
+                                             _stream_ptr(stream)), "priskv_crc32_blocks_dev")
+        return out
+
+    def ranges_dev(self, region, offsets, lengths, out=None, stream=None):
+        import torch
+        n = offsets.numel()
+        if lengths.numel() != n or offsets.dtype != torch.int64 or lengths.dtype != torch.int32:
+            raise ValueError("offsets must be int64 and lengths int32 device tensors of equal length")
+        if out is None:
+            out = torch.empty(n, dtype=torch.int32, device=region.device)
+        _check(lib().priskv_crc32_ranges_dev(self._h, region.data_ptr(), offsets.data_ptr(),
+                                             lengths.data_ptr(), n, out.data_ptr(), _stream_ptr(stream)),
+               "priskv_crc32_ranges_dev")
+        return out
+
+    def fill_splitmix(self, region, seed: int, word_offset: int = 0, stream=None, nbytes=None) -> None:
+        nb = region.numel() * region.element_size() if nbytes is None else nbytes
+        _check(lib().priskv_crc_fill_splitmix_dev(self._h, region.data_ptr(), nb, seed & (2**64 - 1),
+                                                  word_offset, _stream_ptr(stream)),
+               "priskv_crc_fill_splitmix_dev")
+
+    # ---- host-resident (streamed over PCIe)
+    def blocks_host(self, region: np.ndarray, block_size: int, out: Optional[np.ndarray] = None) -> np.ndarray:
+        region = np.ascontiguousarray(region).view(np.uint8).reshape(-1)
+        n = region.size // block_size
+        if out is None:
+            out = np.empty(n, dtype=np.uint32)
+        _check(lib().priskv_crc32_blocks_host(self._h, region.ctypes.data, n, block_size, out.ctypes.data),
+               "priskv_crc32_blocks_host")
+        return out
+
+
+def as_u32(t) -> np.ndarray:
+    """int32 tensor of CRC bit patterns -> numpy uint32."""
+    return t.detach().cpu().numpy().view(np.uint32)

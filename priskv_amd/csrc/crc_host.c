@@ -1,0 +1,155 @@
+/*
+ * crc_host.c -- host side of the PrisKV value-block CRC (C, no HIP).
+ *
+ * 1. priskv_crc32(): the drop-in for server/crc.c:90-109 / server/crc.h:37.
+ *    Bit-exact with the reference (reflected 0xEDB88320, init 0 at :92, no
+ *    final xor at :108) but processes 8 bytes per step with eight tables
+ *    (slice-by-8) instead of the reference's byte-serial table walk
+ *    (:70-88).  Reentrant: the tables are built once under pthread_once
+ *    (SURVEY §8b threading row) and only read afterwards; buf is never
+ *    written or retained.  It stays on the CPU because its callers hash keys
+ *    of <= 1 KiB synchronously on the RDMA completion path
+ *    (server/kv.c:314,408, server/rdma.c:764).
+ *
+ * 2. GF(2) algebra for the GPU path.  With init 0 and no xorout the CRC is a
+ *    linear map, so "advance the register over n zero bytes" (Z_n) is a 32x32
+ *    bit matrix and crc(A||B) = Z_|B|(crc(A)) ^ crc(B).  The GPU kernels need
+ *      - the 64 KiB LDS image of slice-by-4 tables for Z_4 (set A) and for
+ *        Z_(4+row gap) (set B), in the rotated 8-copy layout described in
+ *        DESIGN.md §3 (conflict-free ds_read_b32 for any index pattern);
+ *      - per-lane fold columns: lane l's partial is advanced by
+ *        Z_(16*(G-1-l%G)) before the cross-lane XOR;
+ *      - shift columns Z_(2^k) for combining segment partials.
+ */
+#include <pthread.h>
+#include <stdint.h>
+#include <string.h>
+
+#include "../../include/crc.h"
+#include "../../include/priskv_crc_gpu.h"
+#include "crc_internal.h"
+
+#define POLY 0xEDB88320u
+
+static uint32_t g_slice[8][256];     /* g_slice[k][b]: byte b followed by k zero bytes */
+static uint32_t g_zpow[64][32];      /* columns of Z_(2^k) */
+static pthread_once_t g_once = PTHREAD_ONCE_INIT;
+
+static uint32_t mat_apply(const uint32_t m[32], uint32_t v)
+{
+    uint32_t r = 0;
+    while (v) {
+        int i = __builtin_ctz(v);
+        r ^= m[i];
+        v &= v - 1;
+    }
+    return r;
+}
+
+/* out = a o b (apply b first); out may alias neither input */
+static void mat_compose(uint32_t out[32], const uint32_t a[32], const uint32_t b[32])
+{
+    for (int i = 0; i < 32; i++)
+        out[i] = mat_apply(a, b[i]);
+}
+
+static void host_init(void)
+{
+    for (uint32_t b = 0; b < 256; b++) {
+        uint32_t c = b;
+        for (int k = 0; k < 8; k++)
+            c = (c & 1) ? (c >> 1) ^ POLY : (c >> 1);
+        g_slice[0][b] = c;
+    }
+    for (int k = 1; k < 8; k++)
+        for (int b = 0; b < 256; b++) {
+            uint32_t p = g_slice[k - 1][b];
+            g_slice[k][b] = (p >> 8) ^ g_slice[0][p & 0xff];
+        }
+    /* Z_1: one zero byte through the register */
+    for (int i = 0; i < 32; i++) {
+        uint32_t v = 1u << i;
+        g_zpow[0][i] = g_slice[0][v & 0xff] ^ (v >> 8);
+    }
+    for (int k = 1; k < 64; k++)
+        mat_compose(g_zpow[k], g_zpow[k - 1], g_zpow[k - 1]);
+}
+
+static inline uint32_t load_le32(const uint8_t *p)
+{
+    uint32_t v;
+    memcpy(&v, p, 4);
+    return v; /* x86-64 / aarch64-le hosts */
+}
+
+uint32_t priskv_crc32(uint8_t *buf, uint32_t len)
+{
+    pthread_once(&g_once, host_init);
+    uint32_t crc = 0;
+    const uint8_t *p = buf;
+    while (len >= 8) {
+        uint32_t lo = load_le32(p) ^ crc;
+        uint32_t hi = load_le32(p + 4);
+        crc = g_slice[7][lo & 0xff] ^ g_slice[6][(lo >> 8) & 0xff] ^
+              g_slice[5][(lo >> 16) & 0xff] ^ g_slice[4][lo >> 24] ^ g_slice[3][hi & 0xff] ^
+              g_slice[2][(hi >> 8) & 0xff] ^ g_slice[1][(hi >> 16) & 0xff] ^ g_slice[0][hi >> 24];
+        p += 8;
+        len -= 8;
+    }
+    while (len--)
+        crc = g_slice[0][(crc ^ *p++) & 0xff] ^ (crc >> 8);
+    return crc;
+}
+
+uint32_t priskv_crc32_shift(uint32_t crc, uint64_t nbytes)
+{
+    pthread_once(&g_once, host_init);
+    for (int k = 0; nbytes && crc; k++, nbytes >>= 1)
+        if (nbytes & 1)
+            crc = mat_apply(g_zpow[k], crc);
+    return crc;
+}
+
+uint32_t priskv_crc32_combine(uint32_t crc_a, uint32_t crc_b, uint64_t len_b)
+{
+    return priskv_crc32_shift(crc_a, len_b) ^ crc_b;
+}
+
+/* ---- internal (hidden) builders for the HIP shim ---------------------- */
+
+void prv_shift_columns(uint32_t out[32], uint64_t nbytes)
+{
+    for (int i = 0; i < 32; i++)
+        out[i] = priskv_crc32_shift(1u << i, nbytes);
+}
+
+void prv_lds_image(uint32_t out[PRV_LDS_WORDS], uint32_t gap_bytes)
+{
+    uint32_t za[32], zb[32];
+    prv_shift_columns(za, 4);
+    prv_shift_columns(zb, 4 + (uint64_t)gap_bytes);
+    for (uint32_t idx = 0; idx < 256; idx++)
+        for (uint32_t k = 0; k < 8; k++)
+            for (uint32_t t = 0; t < 4; t++) {
+                /* slot t of copy k holds the table for byte position t of the
+                 * 32-bit register: E_t[idx] = Z(idx << 8t) */
+                out[idx * 64 + 4 * k + t] = mat_apply(za, idx << (8 * t));
+                out[idx * 64 + 32 + 4 * k + t] = mat_apply(zb, idx << (8 * t));
+            }
+}
+
+void prv_fold_columns(uint32_t out[32 * 64], uint32_t group)
+{
+    /* out[i*64 + l] = column i of Z_(16*(G-1-(l%G))), G = group (1..64) */
+    for (uint32_t l = 0; l < 64; l++) {
+        uint64_t dist = 16ull * (group - 1 - (l % group));
+        for (int i = 0; i < 32; i++)
+            out[i * 64 + l] = priskv_crc32_shift(1u << i, dist);
+    }
+}
+
+void prv_sarwate_table(uint32_t out[256])
+{
+    pthread_once(&g_once, host_init);
+    memcpy(out, g_slice[0], sizeof(g_slice[0]));
+}

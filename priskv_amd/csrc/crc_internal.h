@@ -1,0 +1,32 @@
+/* crc_internal.h -- hidden helpers shared by crc_host.c and crc_gpu.hip. */
+#ifndef PRISKV_CRC_INTERNAL_H
+#define PRISKV_CRC_INTERNAL_H
+
+#include <stdint.h>
+
+#if defined(__cplusplus)
+extern "C"
+{
+#endif
+
+#define PRV_HIDDEN __attribute__((visibility("hidden")))
+
+/* LDS image: 256 rows x 64 words (256 B): words [0,32) = set A (Z_4),
+ * words [32,64) = set B (Z_(4+gap)); word 4k+t of a half = table for byte
+ * position t, copy k (k = 0..7).  64 KiB total. */
+#define PRV_LDS_WORDS (256 * 64)
+
+/* wave row: 64 lanes x 16 B */
+#define PRV_ROW_BYTES 1024u
+#define PRV_ROW_GAP (PRV_ROW_BYTES - 16u)
+
+PRV_HIDDEN void prv_lds_image(uint32_t out[PRV_LDS_WORDS], uint32_t gap_bytes);
+PRV_HIDDEN void prv_fold_columns(uint32_t out[32 * 64], uint32_t group);
+PRV_HIDDEN void prv_shift_columns(uint32_t out[32], uint64_t nbytes);
+PRV_HIDDEN void prv_sarwate_table(uint32_t out[256]);
+
+#if defined(__cplusplus)
+}
+#endif
+
+#endif

@@ -1,0 +1,231 @@
+"""GPU parity: libpriskv_crc.so's HIP kernels vs the CPU oracle (bit-exact).
+
+Every call goes through the C ABI (include/priskv_crc_gpu.h) via ctypes.
+Inputs are seeded splitmix64 patterns produced on the device by the
+library's fill kernel, whose bytes are themselves checked against the
+oracle's generator; expected values come from the oracle
+(oracle/crc_oracle.c, pinned to the reference in test_oracle.py) or
+straight from the golden fixture produced by the reference.
+"""
+import numpy as np
+import pytest
+
+import _oracle as O
+
+pytestmark = pytest.mark.gpu
+
+SEED = 0x5EED5EED
+
+
+@pytest.fixture(scope="module")
+def torch_cuda():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return torch
+
+
+@pytest.fixture(scope="module")
+def ctx(torch_cuda):
+    from priskv_amd import CrcContext
+    c = CrcContext(0)
+    yield c
+    c.close()
+
+
+def _region(torch, ctx, nbytes, seed=SEED, word_offset=0, pad=0):
+    t = torch.empty(nbytes + pad + 16, dtype=torch.uint8, device="cuda")
+    ctx.fill_splitmix(t, seed, word_offset, nbytes=nbytes + pad)
+    return t
+
+
+def _u32(t):
+    from priskv_amd import as_u32
+    return as_u32(t)
+
+
+def test_fill_matches_oracle_generator(torch_cuda, ctx):
+    torch = torch_cuda
+    for n, off in ((4096, 0), (1 << 20, 12345), (1000003, 7)):
+        t = torch.empty(n, dtype=torch.uint8, device="cuda")
+        ctx.fill_splitmix(t, SEED, off)
+        torch.cuda.synchronize()
+        assert np.array_equal(t.cpu().numpy(), O.fill_splitmix(n, SEED, off)), (n, off)
+
+
+def test_golden_blocks_on_gpu(torch_cuda, ctx, golden):
+    """The reference's own outputs (fixture) reproduced by the HIP kernels."""
+    torch = torch_cuda
+    for b in golden["blocks"]:
+        bs, nb = b["block_size"], b["nblocks"]
+        t = _region(torch, ctx, bs * nb, golden["seed"], b["word_offset"])
+        out = ctx.blocks_dev(t, bs, nblocks=nb)
+        torch.cuda.synchronize()
+        assert [f"{v:08x}" for v in _u32(out)] == b["crcs"], bs
+
+
+def test_golden_ranges_on_gpu(torch_cuda, ctx, golden):
+    torch = torch_cuda
+    r = golden["ranges"]
+    t = _region(torch, ctx, r["region_bytes"], golden["seed"], r["word_offset"])
+    offs = torch.tensor([it["offset"] for it in r["items"]], dtype=torch.int64, device="cuda")
+    lens = torch.tensor([it["len"] for it in r["items"]], dtype=torch.int32, device="cuda")
+    out = ctx.ranges_dev(t, offs, lens)
+    torch.cuda.synchronize()
+    assert [f"{v:08x}" for v in _u32(out)] == [it["crc"] for it in r["items"]]
+
+
+# block sizes covering every dispatch path and chunking variant:
+#   rows CH=4 (4K, 8K, 12K, 64K, 1M), CH=2 (2K, 6K), CH=1 (1K, 3K, 5K),
+#   small (16..512), generic (odd sizes)
+BLOCK_SIZES = [1024, 2048, 3072, 4096, 5120, 6144, 8192, 12288, 65536, 1 << 20,
+               16, 32, 64, 128, 256, 512, 1, 3, 100, 1000, 4097, 4100, 48]
+NBLOCKS = [1, 2, 7, 63, 64, 65, 129, 1000, 4099]
+
+
+@pytest.mark.parametrize("bs", BLOCK_SIZES)
+def test_blocks_vs_oracle(torch_cuda, ctx, bs):
+    torch = torch_cuda
+    for nb in NBLOCKS:
+        if bs * nb > (64 << 20):
+            continue
+        t = _region(torch, ctx, bs * nb, SEED ^ bs, nb)
+        out = ctx.blocks_dev(t, bs, nblocks=nb)
+        torch.cuda.synchronize()
+        host = t[: bs * nb].cpu().numpy()
+        want = O.crc32_blocks(host, bs, nthreads=8)
+        got = _u32(out)
+        assert np.array_equal(got, want), (bs, nb, np.nonzero(got != want)[0][:8])
+
+
+@pytest.mark.parametrize("misalign", [1, 2, 4, 8, 12])
+def test_unaligned_base(torch_cuda, ctx, misalign):
+    torch = torch_cuda
+    bs, nb = 4096, 97
+    t = _region(torch, ctx, bs * nb + 64, SEED, 3)
+    view = t[misalign: misalign + bs * nb]
+    out = ctx.blocks_dev(view, bs, nblocks=nb)
+    torch.cuda.synchronize()
+    assert np.array_equal(_u32(out), O.crc32_blocks(view.cpu().numpy(), bs))
+
+
+def test_zero_and_ff_blocks(torch_cuda, ctx):
+    torch = torch_cuda
+    for bs in (16, 512, 4096, 65536):
+        z = torch.zeros(bs * 33, dtype=torch.uint8, device="cuda")
+        out = ctx.blocks_dev(z, bs)
+        torch.cuda.synchronize()
+        assert not _u32(out).any()  # init 0 / xorout 0: zero data -> CRC 0
+        f = torch.full((bs * 33,), 0xFF, dtype=torch.uint8, device="cuda")
+        out = ctx.blocks_dev(f, bs)
+        torch.cuda.synchronize()
+        want = O.crc32(b"\xff" * bs)
+        assert (_u32(out) == want).all()
+
+
+def test_single_bit_flips_detected(torch_cuda, ctx):
+    """Each flipped bit changes exactly its own block's CRC by crc(e_bit)."""
+    torch = torch_cuda
+    bs, nb = 4096, 256
+    t = _region(torch, ctx, bs * nb)
+    base = _u32(ctx.blocks_dev(t, bs, nblocks=nb)).copy()
+    rng = np.random.default_rng(1)
+    flips = rng.integers(0, bs * nb * 8, 64)
+    for f in flips:
+        byte, bit = int(f) // 8, int(f) % 8
+        t[byte] ^= (1 << bit)
+    out = _u32(ctx.blocks_dev(t, bs, nblocks=nb))
+    torch.cuda.synchronize()
+    want = O.crc32_blocks(t[: bs * nb].cpu().numpy(), bs)
+    assert np.array_equal(out, want)
+    touched = {int(f) // 8 // bs for f in flips}
+    assert {i for i in range(nb) if out[i] != base[i]} <= touched
+
+
+def test_ranges_vs_oracle(torch_cuda, ctx):
+    torch = torch_cuda
+    n = 8 << 20
+    t = _region(torch, ctx, n, SEED, 99)
+    rng = np.random.default_rng(4)
+    k = 3000
+    lens = rng.integers(0, 70000, k).astype(np.uint32)
+    lens[:10] = [0, 1, 2, 3, 4, 5, 15, 16, 17, 1 << 20]
+    offs = np.array([rng.integers(0, n - int(ln)) for ln in lens], dtype=np.uint64)
+    out = ctx.ranges_dev(t, torch.from_numpy(offs.astype(np.int64)).cuda(),
+                         torch.from_numpy(lens.view(np.int32)).cuda())
+    torch.cuda.synchronize()
+    want = O.crc32_ranges(t[:n].cpu().numpy(), offs, lens)
+    assert np.array_equal(_u32(out), want)
+
+
+@pytest.mark.parametrize("pinned", [False, True])
+def test_blocks_host_streamed(torch_cuda, ctx, pinned):
+    from priskv_amd import host_register, host_unregister
+    bs = 4096
+    nb = (200 << 20) // bs + 3  # > 3 chunks of 64 MiB, ragged tail
+    host = O.fill_splitmix(bs * nb, SEED, 5)
+    if pinned:
+        host_register(host)
+    try:
+        got = ctx.blocks_host(host, bs)
+    finally:
+        if pinned:
+            host_unregister(host)
+    assert np.array_equal(got, O.crc32_blocks(host, bs, nthreads=8))
+
+
+def test_blocks_host_odd_sizes(torch_cuda, ctx):
+    for bs, nb in ((100, 1000), (1 << 20, 5), (64, 7)):
+        host = O.fill_splitmix(bs * nb, SEED, 1)
+        assert np.array_equal(ctx.blocks_host(host, bs), O.crc32_blocks(host, bs))
+
+
+def test_stream_argument(torch_cuda, ctx):
+    torch = torch_cuda
+    s = torch.cuda.Stream()
+    bs, nb = 65536, 300
+    with torch.cuda.stream(s):
+        t = _region(torch, ctx, bs * nb)
+        out = ctx.blocks_dev(t, bs, stream=s)
+    s.synchronize()
+    assert np.array_equal(_u32(out), O.crc32_blocks(t.cpu().numpy()[: bs * nb], bs, nthreads=8))
+
+
+def test_bad_args_on_gpu(torch_cuda, ctx):
+    from priskv_amd.crc import lib
+    L = lib()
+    assert L.priskv_crc32_blocks_dev(ctx.handle, None, 5, 4096, None, None) == -22
+    assert L.priskv_crc32_blocks_dev(ctx.handle, None, 0, 4096, None, None) == 0
+    assert L.priskv_crc32_blocks_dev(ctx.handle, 16, 5, 0, 16, None) == -22
+    import ctypes
+    h = ctypes.c_void_p()
+    assert L.priskv_crc_ctx_create(4096, ctypes.byref(h)) == -19
+
+
+@pytest.mark.slow
+def test_full_config_1M_x_4K(torch_cuda, ctx):
+    """BASELINE config 2: 1 Mi x 4 KiB = 4 GiB device-resident, every block
+    checked against the oracle run on a D2H copy."""
+    torch = torch_cuda
+    bs, nb = 4096, 1 << 20
+    t = torch.empty(bs * nb, dtype=torch.uint8, device="cuda")
+    ctx.fill_splitmix(t, SEED, 0)
+    out = ctx.blocks_dev(t, bs)
+    torch.cuda.synchronize()
+    host = t.cpu().numpy()
+    want = O.crc32_blocks(host, bs, nthreads=16)
+    assert np.array_equal(_u32(out), want)
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("bs", [65536, 1 << 20])
+def test_full_sweep_4GiB(torch_cuda, ctx, bs):
+    """BASELINE config 3 (sweep): 4 GiB of 64 KiB or 1 MiB blocks, all checked."""
+    torch = torch_cuda
+    nb = (4 << 30) // bs
+    t = torch.empty(bs * nb, dtype=torch.uint8, device="cuda")
+    ctx.fill_splitmix(t, SEED ^ bs, 0)
+    out = ctx.blocks_dev(t, bs)
+    torch.cuda.synchronize()
+    want = O.crc32_blocks(t.cpu().numpy(), bs, nthreads=16)
+    assert np.array_equal(_u32(out), want)

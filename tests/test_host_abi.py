@@ -1,0 +1,180 @@
+"""CPU-side checks of the product library (no GPU needed).
+
+* libpriskv_crc.so loads and exports exactly the functions include/*.h declare;
+* priskv_crc32 (the drop-in for server/crc.h:37, host slice-by-8) is bit-exact
+  with the golden vectors and the oracle;
+* the static drop-in archive links into a C program written against
+  include/crc.h the way server/kv.c calls it (server/kv.c:314);
+* GF(2) shift/combine identities the GPU fold relies on.
+"""
+import ctypes
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+import _oracle as O
+from priskv_amd import crc as C
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+INCLUDE = os.path.join(ROOT, "include")
+LIBDIR = os.path.join(ROOT, "priskv_amd", "lib")
+
+
+def _declared_functions():
+    names = set()
+    for h in sorted(os.listdir(INCLUDE)):
+        if not h.endswith(".h"):
+            continue
+        src = open(os.path.join(INCLUDE, h)).read()
+        src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+        src = re.sub(r"//.*", "", src)
+        for m in re.finditer(r"\b([A-Za-z_][A-Za-z0-9_]*)\s*\([^;{]*\)\s*;", src):
+            names.add(m.group(1))
+    return names
+
+
+def test_library_exports_every_declared_symbol():
+    L = C.lib()
+    declared = _declared_functions()
+    assert "priskv_crc32" in declared and "priskv_crc32_blocks_dev" in declared
+    for name in declared:
+        assert hasattr(L, name), name
+    bound = {s[0] for s in C.SIGNATURES}
+    assert declared == bound, declared ^ bound
+
+
+def test_library_exports_nothing_else():
+    out = subprocess.run(["nm", "-D", "--defined-only", C.LIB_PATH], capture_output=True, text=True,
+                         check=True).stdout
+    exported = {ln.split()[-1] for ln in out.splitlines() if " T " in ln}
+    assert exported == _declared_functions(), exported ^ _declared_functions()
+
+
+def test_version():
+    assert "gfx950" in C.version()
+
+
+def test_priskv_crc32_golden(golden):
+    for s in golden["strings"]:
+        data = bytes.fromhex(s["hex"]) if s["hex"] is not None else bytes([s["repeat"]["byte"]]) * s["repeat"]["n"]
+        assert C.priskv_crc32(data) == int(s["crc"], 16)
+    for c in golden["lengths"]:
+        kind, n = c["pattern"], c["len"]
+        if kind == "zero":
+            data = b"\x00" * n
+        elif kind == "ff":
+            data = b"\xff" * n
+        elif kind == "counter":
+            data = bytes(i & 0xFF for i in range(n))
+        else:
+            data = O.fill_splitmix(n, golden["seed"]).tobytes()
+        assert C.priskv_crc32(data) == int(c["crc"], 16), (kind, n)
+
+
+def test_priskv_crc32_vs_oracle_unaligned():
+    rng = np.random.default_rng(5)
+    buf = rng.integers(0, 256, 20000, dtype=np.uint8)
+    for _ in range(500):
+        off = int(rng.integers(0, 64))
+        n = int(rng.integers(0, 4000))
+        s = buf[off:off + n]
+        assert C.priskv_crc32(s) == O.crc32(s)
+
+
+def test_priskv_crc32_threads():
+    # reentrancy (SURVEY §8b threading row; server/test/test_kv_mt.c uses 4 threads)
+    from concurrent.futures import ThreadPoolExecutor
+    rng = np.random.default_rng(9)
+    bufs = [rng.integers(0, 256, int(rng.integers(1, 1025)), dtype=np.uint8).tobytes() for _ in range(400)]
+    want = [O.crc32(b) for b in bufs]
+    with ThreadPoolExecutor(8) as ex:
+        got = list(ex.map(C.priskv_crc32, bufs))
+    assert got == want
+
+
+def test_shift_and_combine():
+    rng = np.random.default_rng(21)
+    for _ in range(50):
+        a = rng.integers(0, 256, int(rng.integers(0, 3000)), dtype=np.uint8).tobytes()
+        b = rng.integers(0, 256, int(rng.integers(0, 3000)), dtype=np.uint8).tobytes()
+        assert C.crc32_combine(O.crc32(a), O.crc32(b), len(b)) == O.crc32(a + b)
+        # shift == feeding zero bytes
+        z = int(rng.integers(0, 5000))
+        assert C.crc32_shift(O.crc32(a), z) == O.crc32(a + b"\x00" * z)
+    # huge shifts compose
+    c = 0xDEADBEEF
+    assert C.crc32_shift(C.crc32_shift(c, 1 << 40), 12345) == C.crc32_shift(c, (1 << 40) + 12345)
+
+
+def test_static_dropin_links_like_kv_c(tmp_path):
+    """Compile a caller against include/crc.h exactly as server/kv.c:314 calls it
+    (`uint32_t crc = priskv_crc32(key, keylen);` with uint8_t *key, uint16_t keylen)
+    and link it against libpriskv_crc_host.a -- the object server/Makefile would
+    link in place of crc.o (server/Makefile:32-35)."""
+    archive = os.path.join(LIBDIR, "libpriskv_crc_host.a")
+    assert os.path.exists(archive)
+    src = tmp_path / "caller.c"
+    src.write_text(
+        '#include <stdio.h>\n#include <string.h>\n#include "crc.h"\n'
+        "int main(void) {\n"
+        "  uint8_t key[] = \"123456789\"; uint16_t keylen = 9;\n"
+        "  uint32_t crc = priskv_crc32(key, keylen);\n"
+        "  uint32_t bucket = crc % 1000003u;\n"
+        "  printf(\"%08x %u\\n\", crc, bucket);\n"
+        "  return crc == 0x2dfd2d88u ? 0 : 1;\n}\n")
+    exe = tmp_path / "caller"
+    subprocess.run(["gcc", "-O2", "-Wall", "-Werror", f"-I{INCLUDE}", str(src), archive, "-lpthread", "-o",
+                    str(exe)], check=True)
+    r = subprocess.run([str(exe)], capture_output=True, text=True)
+    assert r.returncode == 0, r.stdout
+    assert r.stdout.split()[0] == "2dfd2d88"
+    # the archive defines priskv_crc32 and no unprefixed globals that could clash
+    syms = subprocess.run(["nm", "--defined-only", "-g", archive], capture_output=True, text=True).stdout
+    gl = {ln.split()[-1] for ln in syms.splitlines() if re.match(r"^[0-9a-f]+ [TDBR] ", ln)}
+    assert "priskv_crc32" in gl
+    assert all(s.startswith(("priskv_crc", "prv_")) for s in gl), gl
+
+
+def test_header_prototype_matches_reference():
+    """The prototype text is the reference's server/crc.h:37 (checked when the
+    reference tree is mounted, i.e. in the dev container)."""
+    ref = "/root/reference/server/crc.h"
+    ours = open(os.path.join(INCLUDE, "crc.h")).read()
+    assert "uint32_t priskv_crc32(uint8_t *buf, uint32_t len);" in ours
+    assert "#ifndef __PRISKV_SERVER_CRC__" in ours
+    if not os.path.exists(ref):
+        pytest.skip("reference not mounted")
+    assert "uint32_t priskv_crc32(uint8_t *buf, uint32_t len);" in open(ref).read()
+
+
+def test_batch_entry_points_reject_bad_args_without_gpu():
+    L = C.lib()
+    # NULL context is rejected before any HIP call
+    assert L.priskv_crc32_blocks_dev(None, 1, 1, 4096, 1, None) == -22
+    assert L.priskv_crc32_ranges_dev(None, 1, 1, 1, 1, 1, None) == -22
+    assert L.priskv_crc32_blocks_host(None, 1, 1, 4096, 1) == -22
+    assert L.priskv_crc_fill_splitmix_dev(None, 16, 16, 0, 0, None) == -22
+    assert L.priskv_crc32_blocks_path(None, 1, 4096) == -22
+    assert L.priskv_crc32_blocks_path(16, 1, 0) == -22
+
+
+def test_path_selection():
+    assert C.blocks_path(4096, 10, 4096) == "rows"
+    assert C.blocks_path(4096, 10, 1 << 20) == "rows"
+    assert C.blocks_path(4096, 10, 3072) == "rows"
+    assert C.blocks_path(4096, 10, 256) == "small"
+    assert C.blocks_path(4096, 10, 16) == "small"
+    assert C.blocks_path(4096, 10, 100) == "generic"
+    assert C.blocks_path(4097, 10, 4096) == "generic"   # unaligned base
+    assert C.blocks_path(4104, 10, 4096) == "generic"   # 8-byte aligned only
+
+
+def test_ctx_create_without_gpu_is_enodev():
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    h = ctypes.c_void_p()
+    assert C.lib().priskv_crc_ctx_create(0, ctypes.byref(h)) == -19
