@@ -1,0 +1,267 @@
+// crc_explore.hip -- design-space explorer for the hot kernel (not product).
+//
+// Builds the same device code as the library (priskv_amd/csrc/crc_device.inc)
+// and times, interleaved round-robin in ONE process (CDNA guide §5.4 rule 24):
+//   * read-only roofs with the hot kernel's exact access pattern and with a
+//     plain grid-stride stream (what HBM gives this pattern with no hashing);
+//   * crc_rows_kernel variants: prefetch depth (NBUF), cache policy (AUX),
+//     block assignment (contiguous per wave vs cyclic), workgroups per CU;
+// checking every CRC variant bit-exactly against the first one.
+// Usage: crc_explore [block_size] [nblocks] [rounds]
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <vector>
+
+#include "../priskv_amd/csrc/crc_internal.h"
+
+namespace {
+#include "../priskv_amd/csrc/crc_device.inc"
+
+// read-only roof with the rows kernel's loop and addressing (same loads, no hashing)
+template <int G, int CH, int NBUF, int AUX>
+__global__ __launch_bounds__(kThreads, 2) void roof_rows(const uint8_t *__restrict__ base, uint64_t ngroups,
+                                                         uint32_t block_size, const uint32_t *, const uint32_t *,
+                                                         uint32_t *__restrict__ out)
+{
+    constexpr int NB = 64 / G, RB = 16 * G;
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint64_t W = (uint64_t)gridDim.x * kWaves;
+    const uint64_t wid = (uint64_t)blockIdx.x * kWaves + wave;
+    const uint64_t g0 = uniform64(ngroups * wid / W);
+    const uint64_t ng = ngroups * (wid + 1) / W - g0;
+    if (ng == 0)
+        return;
+    const uint32_t cps = block_size / (CH * RB);
+    const uint32_t nq = __builtin_amdgcn_readfirstlane((uint32_t)ng * cps);
+    const uint32_t span = (NB - 1) * block_size + CH * RB;
+    const uint32_t voff = (uint32_t)(lane / G) * block_size + (uint32_t)(lane % G) * 16;
+    const uint64_t gstride = (uint64_t)NB * block_size;
+    const uint32_t cstride = CH * RB;
+    const uint8_t *pp = base + g0 * gstride;
+    uint32_t pc = 0, pq = 0;
+    auto advance = [&]() {
+        if (pq + 1 < nq) {
+            pq++;
+            if (++pc == cps) {
+                pc = 0;
+                pp += gstride - (uint64_t)(cps - 1) * cstride;
+            } else {
+                pp += cstride;
+            }
+        }
+    };
+    v4u buf[NBUF][CH];
+#pragma unroll
+    for (int j = 0; j < NBUF - 1; j++) {
+        load_chunk<CH, RB, AUX>(buf[j], pp, span, voff);
+        advance();
+    }
+    uint32_t acc = 0, q = 0;
+    for (; q + NBUF <= nq; q += NBUF) {
+#pragma unroll
+        for (int j = 0; j < NBUF; j++) {
+            load_chunk<CH, RB, AUX>(buf[(j + NBUF - 1) % NBUF], pp, span, voff);
+            advance();
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int k = 0; k < CH; k++)
+                acc ^= buf[j][k].x ^ buf[j][k].y ^ buf[j][k].z ^ buf[j][k].w;
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < NBUF - 1; j++) {
+        if (q + j >= nq)
+            break;
+#pragma unroll
+        for (int k = 0; k < CH; k++)
+            acc ^= buf[j][k].x ^ buf[j][k].y ^ buf[j][k].z ^ buf[j][k].w;
+    }
+    out[wid * 64 + lane] = acc;
+}
+
+__global__ __launch_bounds__(256) void roof_gridstride(const v4u *__restrict__ p, uint64_t n16,
+                                                       uint32_t *__restrict__ out)
+{
+    uint32_t acc = 0;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    for (; i + 3 * stride < n16; i += 4 * stride) {
+        v4u a = __builtin_nontemporal_load(p + i), b = __builtin_nontemporal_load(p + i + stride),
+            c = __builtin_nontemporal_load(p + i + 2 * stride), d = __builtin_nontemporal_load(p + i + 3 * stride);
+        acc ^= a.x ^ a.y ^ a.z ^ a.w ^ b.x ^ b.y ^ b.z ^ b.w ^ c.x ^ c.y ^ c.z ^ c.w ^ d.x ^ d.y ^ d.z ^ d.w;
+    }
+    for (; i < n16; i += stride) {
+        v4u a = p[i];
+        acc ^= a.x ^ a.y ^ a.z ^ a.w;
+    }
+    out[(uint64_t)blockIdx.x * blockDim.x + threadIdx.x] = acc;
+}
+} // namespace
+
+#define CK(x)                                                                                      \
+    do {                                                                                           \
+        hipError_t e_ = (x);                                                                       \
+        if (e_ != hipSuccess) {                                                                    \
+            fprintf(stderr, "%s:%d %s -> %s\n", __FILE__, __LINE__, #x, hipGetErrorString(e_));   \
+            exit(2);                                                                               \
+        }                                                                                          \
+    } while (0)
+
+struct Variant {
+    const char *name;
+    bool is_crc;
+    int G, CH, wg_per_cu;
+    void (*launch)(dim3, hipStream_t, const uint8_t *, uint64_t, uint32_t, const uint32_t *, const uint32_t *,
+                   uint32_t *);
+    std::vector<float> ms;
+};
+
+#define VARIANT(KERN, ISCRC, G, CH, NB, AUX, WGPC)                                                          \
+    Variant{#KERN " G" #G " CH" #CH " NBUF" #NB " AUX" #AUX " wg/cu" #WGPC, ISCRC, G, CH, WGPC,            \
+            [](dim3 g, hipStream_t s, const uint8_t *b, uint64_t n, uint32_t bs, const uint32_t *img,        \
+               const uint32_t *fold, uint32_t *o) {                                                         \
+                hipLaunchKernelGGL((KERN<G, CH, NB, AUX>), g, dim3(kThreads), 0, s, b, n, bs, img, fold, o); \
+            }, {}}
+#define CRC_VARIANT(G, CH, NB, AUX, WGPC) VARIANT(crc_rows_kernel, true, G, CH, NB, AUX, WGPC)
+#define ROOF_VARIANT(G, CH, NB, AUX, WGPC) VARIANT(roof_rows, false, G, CH, NB, AUX, WGPC)
+
+int main(int argc, char **argv)
+{
+    const uint32_t bs = argc > 1 ? (uint32_t)atoi(argv[1]) : 4096;
+    const uint64_t nb = argc > 2 ? strtoull(argv[2], 0, 0) : (1ull << 32) / bs;
+    const int rounds = argc > 3 ? atoi(argv[3]) : 5;
+    int ncu = 0;
+    CK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, 0));
+    hipDeviceProp_t prop;
+    CK(hipGetDeviceProperties(&prop, 0));
+    printf("device %s  CUs %d  block %u x %llu = %.2f GiB\n", prop.gcnArchName, ncu, bs, (unsigned long long)nb,
+           (double)bs * nb / (1 << 30));
+
+    uint8_t *d;
+    uint32_t *d_img[65] = {}, *d_fold[65] = {}, *d_out, *d_ref, *d_sink;
+    for (int G = 16; G <= 64; G *= 2) {
+        std::vector<uint32_t> img(PRV_LDS_WORDS), fold(2048);
+        prv_lds_image(img.data(), 16u * G - 16u);
+        prv_fold_columns(fold.data(), G);
+        CK(hipMalloc(&d_img[G], img.size() * 4));
+        CK(hipMalloc(&d_fold[G], fold.size() * 4));
+        CK(hipMemcpy(d_img[G], img.data(), img.size() * 4, hipMemcpyHostToDevice));
+        CK(hipMemcpy(d_fold[G], fold.data(), fold.size() * 4, hipMemcpyHostToDevice));
+    }
+    CK(hipMalloc(&d, (size_t)bs * nb));
+    CK(hipMalloc(&d_out, nb * 4));
+    CK(hipMalloc(&d_ref, nb * 4));
+    CK(hipMalloc(&d_sink, (size_t)ncu * 16 * 1024 * 4));
+    hipLaunchKernelGGL(fill_splitmix_kernel, dim3(ncu * 16), dim3(256), 0, 0, d, (uint64_t)bs * nb, 0x5EED5EEDull,
+                       0ull);
+    CK(hipDeviceSynchronize());
+
+    std::vector<Variant> all;
+    all.push_back(CRC_VARIANT(16, 8, 2, 2, 2));
+    all.push_back(CRC_VARIANT(64, 4, 2, 2, 2));
+    all.push_back(CRC_VARIANT(64, 4, 2, 2, 1));
+    all.push_back(CRC_VARIANT(64, 2, 3, 2, 2));
+    all.push_back(CRC_VARIANT(64, 8, 2, 2, 1));
+    all.push_back(CRC_VARIANT(32, 4, 2, 2, 2));
+    all.push_back(CRC_VARIANT(32, 8, 2, 2, 1));
+    all.push_back(CRC_VARIANT(16, 4, 2, 2, 2));
+    all.push_back(CRC_VARIANT(16, 4, 3, 2, 2));
+    all.push_back(CRC_VARIANT(16, 8, 2, 2, 1));
+    all.push_back(CRC_VARIANT(16, 8, 2, 0, 2));
+    all.push_back(CRC_VARIANT(16, 16, 2, 2, 1));
+    all.push_back(ROOF_VARIANT(64, 4, 2, 2, 2));
+    all.push_back(ROOF_VARIANT(16, 8, 2, 2, 2));
+    all.push_back(ROOF_VARIANT(16, 8, 2, 2, 1));
+    all.push_back(ROOF_VARIANT(64, 4, 3, 2, 2));
+    std::vector<Variant> V;
+    for (auto &v : all)
+        if (bs % (uint32_t)(v.CH * 16 * v.G) == 0 && nb % (64 / v.G) == 0)
+            V.push_back(v);
+    Variant gs{"roof gridstride nt", false, 64, 1, 8, nullptr, {}};
+
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    const int iters = 5;
+    bool ok_all = true;
+    for (int r = 0; r < rounds + 1; r++) { // round 0 = warm-up
+        for (size_t vi = 0; vi <= V.size(); vi++) {
+            Variant &v = vi < V.size() ? V[vi] : gs;
+            CK(hipEventRecord(e0, 0));
+            for (int it = 0; it < iters; it++) {
+                if (vi < V.size()) {
+                    const uint64_t ng = nb / (64 / v.G);
+                    const uint64_t want = (ng + kWaves - 1) / kWaves;
+                    const uint32_t grid = (uint32_t)std::min<uint64_t>(want, (uint64_t)ncu * v.wg_per_cu);
+                    v.launch(dim3(grid), 0, d, ng, bs, d_img[v.G], d_fold[v.G], v.is_crc ? d_out : d_sink);
+                } else {
+                    hipLaunchKernelGGL(roof_gridstride, dim3(ncu * 8), dim3(256), 0, 0, (const v4u *)d,
+                                       (uint64_t)bs * nb / 16, d_sink);
+                }
+            }
+            CK(hipEventRecord(e1, 0));
+            CK(hipEventSynchronize(e1));
+            float ms;
+            CK(hipEventElapsedTime(&ms, e0, e1));
+            if (r > 0)
+                v.ms.push_back(ms / iters);
+            if (vi < V.size() && v.is_crc && r == 0) {
+                if (vi == 0)
+                    CK(hipMemcpy(d_ref, d_out, nb * 4, hipMemcpyDeviceToDevice));
+                else {
+                    std::vector<uint32_t> a(nb), b(nb);
+                    CK(hipMemcpy(a.data(), d_ref, nb * 4, hipMemcpyDeviceToHost));
+                    CK(hipMemcpy(b.data(), d_out, nb * 4, hipMemcpyDeviceToHost));
+                    if (memcmp(a.data(), b.data(), nb * 4)) {
+                        printf("MISMATCH in %s\n", v.name);
+                        ok_all = false;
+                    }
+                }
+            }
+        }
+    }
+    const double bytes = (double)bs * nb;
+    V.push_back(gs);
+    for (auto &v : V) {
+        std::sort(v.ms.begin(), v.ms.end());
+        const double med = v.ms[v.ms.size() / 2], mn = v.ms[0];
+        printf("%-40s median %8.4f ms  %7.1f GB/s (best %7.1f)  %.1f%% of 8 TB/s\n", v.name, med, bytes / med / 1e6,
+               bytes / mn / 1e6, 100.0 * bytes / med / 1e6 / 8000.0);
+    }
+    printf("crc variants bit-identical: %s\n", ok_all ? "yes" : "NO");
+    // sustained run of the first (product) variant: per-launch times
+    {
+        const int n = argc > 4 ? atoi(argv[4]) : 300;
+        std::vector<hipEvent_t> ev(n + 1);
+        for (auto &e : ev)
+            CK(hipEventCreate(&e));
+        const uint64_t ng = nb / (64 / V[0].G);
+        const uint64_t want = (ng + kWaves - 1) / kWaves;
+        const uint32_t grid = (uint32_t)std::min<uint64_t>(want, (uint64_t)ncu * V[0].wg_per_cu);
+        CK(hipEventRecord(ev[0], 0));
+        for (int i = 0; i < n; i++) {
+            V[0].launch(dim3(grid), 0, d, ng, bs, d_img[V[0].G], d_fold[V[0].G], d_out);
+            CK(hipEventRecord(ev[i + 1], 0));
+        }
+        CK(hipDeviceSynchronize());
+        std::vector<float> t(n);
+        for (int i = 0; i < n; i++)
+            CK(hipEventElapsedTime(&t[i], ev[i], ev[i + 1]));
+        printf("sustained %s, %d launches, ms per launch by decile of the run:", V[0].name, n);
+        for (int k = 0; k < 10; k++) {
+            float s = 0;
+            for (int i = k * n / 10; i < (k + 1) * n / 10; i++)
+                s += t[i];
+            printf(" %.4f", s / (n / 10));
+        }
+        std::sort(t.begin(), t.end());
+        printf("\n  min %.4f  median %.4f  max %.4f ms\n", t[0], t[n / 2], t[n - 1]);
+    }
+    return ok_all ? 0 : 1;
+}
