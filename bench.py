@@ -112,7 +112,7 @@ def main():
         ctx.blocks_dev(region, bs, out=out, stream=stream)
     torch.cuda.synchronize()
     # The first ~10 launches after idle run up to 40% slow while the device
-    # leaves its idle power state (profiles/r01_clock_ramp.txt); keep stepping,
+    # leaves its idle power state (profiles/r01/clock_ramp.txt); keep stepping,
     # untimed, until >= RAMP_S seconds of back-to-back work have passed so the
     # timed steps see steady-state serving throughput.
     ramp = 0
@@ -211,11 +211,18 @@ def main():
 
 
 def ctx_path(bs, region):
+    """Kernel the library dispatches to (mirrors plan_for() in crc_gpu.hip)."""
     from priskv_amd import blocks_path
     p = blocks_path(region.data_ptr(), 1, bs)
     if p == "rows":
-        r = bs // 1024
-        return f"crc_rows_kernel<{4 if r % 4 == 0 else (2 if r % 2 == 0 else 1)}>"
+        if bs <= 16384 and bs % 4096 == 0:
+            g, ch = 32, 8
+        elif bs <= 16384:
+            g, ch = 16, 4
+        else:
+            r = bs // 1024
+            g, ch = 64, (4 if r % 4 == 0 else (2 if r % 2 == 0 else 1))
+        return f"crc_rows_kernel<G={g},CH={ch},NBUF=2,nt>"
     return f"crc_{p}_kernel"
 
 

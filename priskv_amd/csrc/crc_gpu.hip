@@ -55,7 +55,7 @@ struct priskv_crc_ctx {
     int device;
     int num_cus;
     int max_wgs;               // resident workgroups of the sub-KiB kernel (2 per CU)
-    int rows_wgs_per_cu[3][4]; // [G = 64, 32, 16][CH = 1, 2, 4, 8] workgroups per CU
+    int plan_wgs_per_cu[8];    // resident workgroups per CU of each rows-kernel plan
     uint32_t *d_lds_image[3];  // 64 KiB each: set B gap for G = 64, 32, 16
     uint32_t *d_fold;          // kFoldSets x 2048 words, set j for G = 1 << j
     uint32_t *d_sarwate;       // 256 words
@@ -134,38 +134,66 @@ int launch_generic(const priskv_crc_ctx *ctx, const uint8_t *base, uint64_t n, u
     return herr(hipGetLastError());
 }
 
-// ---- rows kernel configurations -------------------------------------------
-// (G lanes per block, CH rows per chunk); pipeline depth and cache policy are
-// fixed product choices (from tools/crc_explore runs).
-#ifndef PRV_ROWS_NBUF
-#define PRV_ROWS_NBUF 2
-#endif
-#ifndef PRV_ROWS_AUX
-#define PRV_ROWS_AUX 2
-#endif
-// blocks up to this size use G = 16 lanes per block (4 blocks per wave)
-#ifndef PRV_G16_MAX_BLOCK
-#define PRV_G16_MAX_BLOCK (16u << 10)
-#endif
+// ---- rows kernel plans --------------------------------------------------------
+// (G lanes per block, CH rows per chunk, workgroups per CU) by block size,
+// from the tools/crc_explore sweeps recorded in DESIGN.md §5.  Pipeline depth
+// (NBUF = 2) and cache policy (nt) are fixed.
+constexpr int kNbuf = 2;
+constexpr int kAux = 2;
+
+enum PlanId { PLAN_G32_CH8, PLAN_G16_CH4, PLAN_G64_CH4, PLAN_G64_CH2, PLAN_G64_CH1, NPLANS };
+struct Plan {
+    int G, CH, wg_per_cu;
+};
+constexpr Plan kPlans[NPLANS] = {{32, 8, 1}, {16, 4, 2}, {64, 4, 1}, {64, 2, 1}, {64, 1, 1}};
+
+int plan_for(uint32_t bs)
+{
+    if (bs <= (16u << 10) && bs % 4096 == 0)
+        return PLAN_G32_CH8;
+    if (bs <= (16u << 10))
+        return PLAN_G16_CH4;
+    const uint32_t R = bs / PRV_ROW_BYTES;
+    return R % 4 == 0 ? PLAN_G64_CH4 : (R % 2 == 0 ? PLAN_G64_CH2 : PLAN_G64_CH1);
+}
 
 template <int G, int CH>
-int launch_rows_cfg(const priskv_crc_ctx *ctx, const uint8_t *base, uint64_t ngroups, uint32_t bs, uint32_t *out,
-                    hipStream_t s)
+const void *plan_kernel()
 {
-    const int gi = G == 64 ? 0 : (G == 32 ? 1 : 2);
-    const int occ = ctx->rows_wgs_per_cu[gi][CH == 8 ? 3 : (CH == 4 ? 2 : (CH == 2 ? 1 : 0))];
-    const uint64_t max_wgs = (uint64_t)ctx->num_cus * (occ > 0 ? occ : 1);
-    const uint64_t cps = bs / (CH * 16u * G);
+    return reinterpret_cast<const void *>(&crc_rows_kernel<G, CH, kNbuf, kAux>);
+}
+
+const void *plan_fn(int p)
+{
+    switch (p) {
+    case PLAN_G32_CH8: return plan_kernel<32, 8>();
+    case PLAN_G16_CH4: return plan_kernel<16, 4>();
+    case PLAN_G64_CH4: return plan_kernel<64, 4>();
+    case PLAN_G64_CH2: return plan_kernel<64, 2>();
+    default: return plan_kernel<64, 1>();
+    }
+}
+
+int launch_plan(const priskv_crc_ctx *ctx, int p, const uint8_t *base, uint64_t ngroups, uint32_t bs, uint32_t *out,
+                hipStream_t s)
+{
+    const Plan &P = kPlans[p];
+    const int gi = P.G == 64 ? 0 : (P.G == 32 ? 1 : 2);
+    const uint64_t max_wgs = (uint64_t)ctx->num_cus * ctx->plan_wgs_per_cu[p];
+    const uint64_t nb_per_group = 64 / P.G;
+    const uint64_t cps = bs / ((uint64_t)P.CH * 16u * P.G);
     // the kernel counts a wave's chunks in 32 bits: cap groups per launch
     const uint64_t cap = max_wgs * kWaves * ((1ull << 31) / cps - 1);
     for (uint64_t done = 0; done < ngroups;) {
-        const uint64_t n = (ngroups - done < cap) ? ngroups - done : cap;
+        uint64_t n = (ngroups - done < cap) ? ngroups - done : cap;
         const uint64_t want = (n + kWaves - 1) / kWaves;
         const uint32_t grid = (uint32_t)(want < max_wgs ? want : max_wgs);
-        hipLaunchKernelGGL((crc_rows_kernel<G, CH, PRV_ROWS_NBUF, PRV_ROWS_AUX>), dim3(grid), dim3(kThreads), 0, s,
-                           base + done * (64 / G) * (uint64_t)bs, n, bs, ctx->d_lds_image[gi],
-                           ctx->d_fold + log2u(G) * 2048, out + done * (64 / G));
-        if (int rc = herr(hipGetLastError()))
+        const uint8_t *b = base + done * nb_per_group * bs;
+        uint32_t *o = out + done * nb_per_group;
+        const uint32_t *img = ctx->d_lds_image[gi];
+        const uint32_t *fold = ctx->d_fold + log2u(P.G) * 2048;
+        void *args[] = {(void *)&b, (void *)&n, (void *)&bs, (void *)&img, (void *)&fold, (void *)&o};
+        if (int rc = herr(hipLaunchKernel(plan_fn(p), dim3(grid), dim3(kThreads), args, 0, s)))
             return rc;
         done += n;
     }
@@ -175,26 +203,18 @@ int launch_rows_cfg(const priskv_crc_ctx *ctx, const uint8_t *base, uint64_t ngr
 int launch_rows(const priskv_crc_ctx *ctx, const uint8_t *base, uint64_t nblocks, uint32_t bs, uint32_t *out,
                 hipStream_t s)
 {
-    // 4-block groups with 16 lanes per block for small value blocks ...
-    uint64_t head = 0;
-    if (bs <= PRV_G16_MAX_BLOCK && nblocks >= 4) {
-        head = nblocks & ~(uint64_t)3;
-        const int rc = (bs % 2048 == 0) ? launch_rows_cfg<16, 8>(ctx, base, head / 4, bs, out, s)
-                                        : launch_rows_cfg<16, 4>(ctx, base, head / 4, bs, out, s);
-        if (rc)
+    const int p = plan_for(bs);
+    const uint64_t per = 64 / kPlans[p].G; // blocks per wave group
+    const uint64_t head = nblocks - nblocks % per;
+    if (head)
+        if (int rc = launch_plan(ctx, p, base, head / per, bs, out, s))
             return rc;
-    }
-    // ... one wave per block for large blocks and for the ragged tail
-    const uint64_t n = nblocks - head;
-    if (!n)
+    if (head == nblocks)
         return 0;
+    // ragged tail (< per blocks): one wave per block
     const uint32_t R = bs / PRV_ROW_BYTES;
-    const uint8_t *b = base + head * (uint64_t)bs;
-    if (R % 4 == 0)
-        return launch_rows_cfg<64, 4>(ctx, b, n, bs, out + head, s);
-    if (R % 2 == 0)
-        return launch_rows_cfg<64, 2>(ctx, b, n, bs, out + head, s);
-    return launch_rows_cfg<64, 1>(ctx, b, n, bs, out + head, s);
+    const int pt = R % 4 == 0 ? PLAN_G64_CH4 : (R % 2 == 0 ? PLAN_G64_CH2 : PLAN_G64_CH1);
+    return launch_plan(ctx, pt, base + head * (uint64_t)bs, nblocks - head, bs, out + head, s);
 }
 
 int launch_blocks(const priskv_crc_ctx *ctx, const uint8_t *base, uint64_t nblocks, uint32_t bs,
@@ -224,30 +244,17 @@ int launch_blocks(const priskv_crc_ctx *ctx, const uint8_t *base, uint64_t nbloc
     return launch_generic(ctx, base, nblocks, bs, bs, nullptr, nullptr, out, s);
 }
 
-// resident workgroups per CU for every rows-kernel configuration (VGPR and
-// LDS limits as the runtime sees them), capped by PRV_ROWS_WG_PER_CU
-#ifndef PRV_ROWS_WG_PER_CU
-#define PRV_ROWS_WG_PER_CU 2
-#endif
-template <int G, int CH>
-int occ_of(int *dst)
-{
-    int n = 0;
-    hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
-        &n, reinterpret_cast<const void *>(&crc_rows_kernel<G, CH, PRV_ROWS_NBUF, PRV_ROWS_AUX>), kThreads, 0);
-    if (e != hipSuccess)
-        return herr(e);
-    *dst = n < 1 ? 1 : (n > PRV_ROWS_WG_PER_CU ? PRV_ROWS_WG_PER_CU : n);
-    return 0;
-}
-
+// resident workgroups per CU of every plan: the plan's choice, capped by
+// what the runtime can actually co-schedule (VGPR / LDS limits)
 int rows_occupancy(priskv_crc_ctx *c)
 {
-    int rc;
-    if ((rc = occ_of<64, 1>(&c->rows_wgs_per_cu[0][0])) || (rc = occ_of<64, 2>(&c->rows_wgs_per_cu[0][1])) ||
-        (rc = occ_of<64, 4>(&c->rows_wgs_per_cu[0][2])) || (rc = occ_of<16, 4>(&c->rows_wgs_per_cu[2][2])) ||
-        (rc = occ_of<16, 8>(&c->rows_wgs_per_cu[2][3])))
-        return rc;
+    for (int p = 0; p < NPLANS; p++) {
+        int n = 0;
+        hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, plan_fn(p), kThreads, 0);
+        if (e != hipSuccess)
+            return herr(e);
+        c->plan_wgs_per_cu[p] = n < 1 ? 1 : (n < kPlans[p].wg_per_cu ? n : kPlans[p].wg_per_cu);
+    }
     return 0;
 }
 

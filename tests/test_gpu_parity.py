@@ -75,11 +75,13 @@ def test_golden_ranges_on_gpu(torch_cuda, ctx, golden):
     assert [f"{v:08x}" for v in _u32(out)] == [it["crc"] for it in r["items"]]
 
 
-# block sizes covering every dispatch path and chunking variant:
-#   rows CH=4 (4K, 8K, 12K, 64K, 1M), CH=2 (2K, 6K), CH=1 (1K, 3K, 5K),
-#   small (16..512), generic (odd sizes)
-BLOCK_SIZES = [1024, 2048, 3072, 4096, 5120, 6144, 8192, 12288, 65536, 1 << 20,
-               16, 32, 64, 128, 256, 512, 1, 3, 100, 1000, 4097, 4100, 48]
+# block sizes covering every dispatch path and rows-kernel plan
+# (priskv_amd/csrc/crc_gpu.hip plan_for):
+#   G32/CH8 (4K, 8K, 12K, 16K), G16/CH4 (1K, 2K, 3K, 5K, 6K),
+#   G64/CH4 (20K, 64K, 1M), G64/CH2 (18K), G64/CH1 (17K, 33K),
+#   sub-KiB (16..512), generic (odd sizes / 16-B multiples that are not powers of two)
+BLOCK_SIZES = [1024, 2048, 3072, 4096, 5120, 6144, 8192, 12288, 16384, 17408, 18432, 20480, 33792,
+               65536, 1 << 20, 16, 32, 64, 128, 256, 512, 1, 3, 100, 1000, 4097, 4100, 48]
 NBLOCKS = [1, 2, 7, 63, 64, 65, 129, 1000, 4099]
 
 
