@@ -85,10 +85,17 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus and rank == 0:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    # one process per GPU; modulo only matters for a multi-rank rehearsal on a
+    # one-GPU box (PRISKV_BENCH_BACKEND=gloo), never on the 8-GPU node
+    gpu = local % max(1, torch.cuda.device_count())
+    torch.cuda.set_device(gpu)
+    dev = torch.device("cuda", gpu)
+    backend = os.environ.get("PRISKV_BENCH_BACKEND", "nccl")  # nccl == RCCL on ROCm
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
 
     from priskv_amd import CrcContext, as_u32
 
@@ -100,10 +107,13 @@ def main():
         bs = args.block_size
     if args.nblocks:
         nb = args.nblocks
-    ctx = CrcContext(local)
+    from priskv_amd.shard import max_over_ranks, shard_blocks, shard_word_offset
+    ctx = CrcContext(gpu)
+    # weak scaling: the global region has world * nb blocks; this rank's shard
+    # is its contiguous range of them (no data-path collective)
+    first, nb = shard_blocks(world * nb, rank, world)
     region = torch.empty(bs * nb, dtype=torch.uint8, device=dev)
-    # this rank's shard = blocks [rank*nb, (rank+1)*nb) of one global region
-    ctx.fill_splitmix(region, SEED, word_offset=rank * (bs * nb // 8))
+    ctx.fill_splitmix(region, SEED, word_offset=shard_word_offset(first, bs))
     out = torch.empty(nb, dtype=torch.int32, device=dev)
     stream = torch.cuda.current_stream()
     torch.cuda.synchronize()
@@ -153,10 +163,7 @@ def main():
     elapsed = t1 - t0
     kernel_ms = ev0.elapsed_time(ev1) / args.steps  # launches back-to-back on `stream`
 
-    el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(el, op=dist.ReduceOp.MAX)
-    elapsed_max = float(el.item())
+    elapsed_max = max_over_ranks(elapsed, device=dev)
 
     total_bytes = bs * nb * world
     value = total_bytes * args.steps / elapsed_max / 2**30
@@ -204,6 +211,15 @@ def main():
         if not ok:
             bad = np.nonzero(cpu_crc != gpu_crc)[0]
             result["parity"]["first_mismatch"] = int(bad[0])
+    elif world > 1:
+        # every rank spot-checks the start of its own shard against the oracle
+        # (untimed); the flags are min-reduced so rank 0 reports all ranks
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        import _oracle as O
+        nsamp = max(1, min(nb, (64 << 20) // bs))
+        ok = np.array_equal(O.crc32_blocks(region[: nsamp * bs].cpu().numpy(), bs, nthreads=8), as_u32(out[:nsamp]))
+        all_ok = max_over_ranks(0.0 if ok else 1.0, device=dev) == 0.0
+        result["parity"] = {"checked_blocks_per_rank": nsamp, "bit_exact": bool(all_ok)}
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:
