@@ -67,6 +67,18 @@ int priskv_crc32_ranges_dev(const priskv_crc_ctx *ctx, const void *d_base,
                             const uint64_t *d_offsets, const uint32_t *d_lengths, uint64_t n,
                             uint32_t *d_out, void *stream);
 
+/* Host-resident per-value extents -- the memfile scrub at recovery
+ * (server/kv.c:824-875 walks the keys; each live value is valuelen bytes at
+ * value_off inside the value region, server/memory.h:50-51).  The kernel
+ * reads only the extents' bytes, straight from the host mapping over PCIe
+ * (zero-copy): h_base must be registered (priskv_crc_host_register) or
+ * pinned, else it is registered for the duration of the call.  h_offsets /
+ * h_lengths / h_out are host arrays of n entries; every extent must lie in
+ * [0, region_bytes) (-EINVAL otherwise).  Synchronous. */
+int priskv_crc32_ranges_host(priskv_crc_ctx *ctx, const void *h_base, uint64_t region_bytes,
+                             const uint64_t *h_offsets, const uint32_t *h_lengths, uint64_t n,
+                             uint32_t *h_out);
+
 /* Host-resident batch (the RDMA-registered value buffer / the memfile
  * mapping): streams the blocks over PCIe in chunks on several HIP streams,
  * overlapping H2D copies, kernels and the small D2H of results; synchronous.
@@ -95,10 +107,9 @@ int priskv_crc_fill_splitmix_dev(const priskv_crc_ctx *ctx, void *d_dst, uint64_
                                  uint64_t seed, uint64_t word_offset, void *stream);
 
 /* Which kernel a (d_base, block_size) batch dispatches to: 1 = rows (block
- * a multiple of 1 KiB, one wave per block), 2 = rows, cooperative (blocks
- * > 64 KiB: the waves of one workgroup split a block), 3 = sub-KiB
- * power-of-two blocks, 4 = generic (any size / alignment).  For tests and
- * benchmarks; -EINVAL for invalid arguments. */
+ * a multiple of 1 KiB, 16-byte aligned base: G = 16/32/64 lanes per block),
+ * 3 = sub-KiB power-of-two blocks, 4 = generic (any size / alignment); 2 is
+ * reserved.  For tests and benchmarks; -EINVAL for invalid arguments. */
 int priskv_crc32_blocks_path(const void *d_base, uint64_t nblocks, uint32_t block_size);
 
 const char *priskv_crc_version(void);

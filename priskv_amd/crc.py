@@ -44,6 +44,8 @@ SIGNATURES = [
      [_C.c_void_p, _C.c_void_p, _C.c_void_p, _C.c_void_p, _C.c_uint64, _C.c_void_p, _C.c_void_p]),
     ("priskv_crc32_blocks_host", _C.c_int,
      [_C.c_void_p, _C.c_void_p, _C.c_uint64, _C.c_uint32, _C.c_void_p]),
+    ("priskv_crc32_ranges_host", _C.c_int,
+     [_C.c_void_p, _C.c_void_p, _C.c_uint64, _C.c_void_p, _C.c_void_p, _C.c_uint64, _C.c_void_p]),
     ("priskv_crc_host_register", _C.c_int, [_C.c_void_p, _C.c_uint64]),
     ("priskv_crc_host_unregister", _C.c_int, [_C.c_void_p]),
     ("priskv_crc32_shift", _C.c_uint32, [_C.c_uint32, _C.c_uint64]),
@@ -198,6 +200,24 @@ class CrcContext:
         _check(lib().priskv_crc32_blocks_host(self._h, region.ctypes.data, n, block_size, out.ctypes.data),
                "priskv_crc32_blocks_host")
         return out
+
+
+def _ranges_host(self, region: np.ndarray, offsets, lengths, out: Optional[np.ndarray] = None) -> np.ndarray:
+    """Per-value extents of a host region (memfile scrub), zero-copy over PCIe."""
+    region = np.ascontiguousarray(region).view(np.uint8).reshape(-1)
+    offs = np.ascontiguousarray(offsets, dtype=np.uint64)
+    lens = np.ascontiguousarray(lengths, dtype=np.uint32)
+    if offs.shape != lens.shape:
+        raise ValueError("offsets and lengths must have the same length")
+    if out is None:
+        out = np.empty(offs.size, dtype=np.uint32)
+    _check(lib().priskv_crc32_ranges_host(self._h, region.ctypes.data, region.size, offs.ctypes.data,
+                                          lens.ctypes.data, offs.size, out.ctypes.data),
+           "priskv_crc32_ranges_host")
+    return out
+
+
+CrcContext.ranges_host = _ranges_host
 
 
 def as_u32(t) -> np.ndarray:

@@ -68,6 +68,9 @@ struct priskv_crc_ctx {
     uint32_t *d_stage_out[NSTREAM];
     void *h_bounce[NSTREAM];
     uint32_t *h_out_stage[NSTREAM];
+    // host-extent scrub scratch (guarded by lock)
+    size_t scrub_cap;
+    void *d_scrub; // offsets | lengths | crcs
 };
 
 namespace {
@@ -345,6 +348,7 @@ void priskv_crc_ctx_destroy(priskv_crc_ctx *c)
         (void)hipFree(c->d_lds_image[gi]);
     (void)hipFree(c->d_fold);
     (void)hipFree(c->d_sarwate);
+    (void)hipFree(c->d_scrub);
     pthread_mutex_destroy(&c->lock);
     free(c);
 }
@@ -378,8 +382,18 @@ int priskv_crc32_ranges_dev(const priskv_crc_ctx *ctx, const void *d_base, const
     DevGuard g(ctx->device);
     if (!g.ok)
         return -ENODEV;
-    return launch_generic(ctx, (const uint8_t *)d_base, n, 0, 0, d_offsets, d_lengths, d_out,
-                          (hipStream_t)stream);
+    // one wave per extent; the base must be 16-B aligned for the row path
+    // (device allocations are), otherwise the byte-serial generic kernel
+    if ((uintptr_t)d_base & 15)
+        return launch_generic(ctx, (const uint8_t *)d_base, n, 0, 0, d_offsets, d_lengths, d_out,
+                              (hipStream_t)stream);
+    const uint64_t want = (n + kWaves - 1) / kWaves;
+    const uint64_t cap = (uint64_t)ctx->num_cus * 2;
+    const uint32_t grid = (uint32_t)(want < cap ? want : cap);
+    hipLaunchKernelGGL(crc_ranges_kernel, dim3(grid), dim3(kThreads), 0, (hipStream_t)stream,
+                       (const uint8_t *)d_base, n, d_offsets, d_lengths, ctx->d_lds_image[0], ctx->d_fold + 6 * 2048,
+                       ctx->d_sarwate, d_out);
+    return herr(hipGetLastError());
 }
 
 int priskv_crc_fill_splitmix_dev(const priskv_crc_ctx *ctx, void *d_dst, uint64_t nbytes, uint64_t seed,
@@ -414,6 +428,62 @@ int priskv_crc_host_unregister(void *h_base)
     if (!h_base)
         return -EINVAL;
     return herr(hipHostUnregister(h_base));
+}
+
+
+int priskv_crc32_ranges_host(priskv_crc_ctx *ctx, const void *h_base, uint64_t region_bytes,
+                             const uint64_t *h_offsets, const uint32_t *h_lengths, uint64_t n, uint32_t *h_out)
+{
+    if (!ctx)
+        return -EINVAL;
+    if (n == 0)
+        return 0;
+    if (!h_base || !h_offsets || !h_lengths || !h_out || !region_bytes)
+        return -EINVAL;
+    for (uint64_t i = 0; i < n; i++)
+        if (h_offsets[i] > region_bytes || h_lengths[i] > region_bytes - h_offsets[i])
+            return -EINVAL;
+    DevGuard g(ctx->device);
+    if (!g.ok)
+        return -ENODEV;
+    // device view of the host mapping (zero-copy): registered/pinned memory
+    // has one; otherwise register it for this call
+    void *dptr = nullptr;
+    bool temp_reg = false;
+    if (hipHostGetDevicePointer(&dptr, const_cast<void *>(h_base), 0) != hipSuccess || !dptr) {
+        (void)hipGetLastError();
+        if (int rc = herr(hipHostRegister(const_cast<void *>(h_base), region_bytes, hipHostRegisterMapped)))
+            return rc;
+        temp_reg = true;
+        if (int rc = herr(hipHostGetDevicePointer(&dptr, const_cast<void *>(h_base), 0))) {
+            (void)hipHostUnregister(const_cast<void *>(h_base));
+            return rc;
+        }
+    }
+    pthread_mutex_lock(&ctx->lock);
+    int rc = 0;
+    const size_t need = (size_t)n * (8 + 4 + 4);
+    if (ctx->scrub_cap < need) {
+        (void)hipFree(ctx->d_scrub);
+        ctx->d_scrub = nullptr;
+        ctx->scrub_cap = 0;
+        if (!(rc = herr(hipMalloc(&ctx->d_scrub, need))))
+            ctx->scrub_cap = need;
+    }
+    if (!rc) {
+        uint64_t *d_off = (uint64_t *)ctx->d_scrub;
+        uint32_t *d_len = (uint32_t *)(d_off + n);
+        uint32_t *d_crc = d_len + n;
+        if (!(rc = herr(hipMemcpy(d_off, h_offsets, n * 8, hipMemcpyHostToDevice))) &&
+            !(rc = herr(hipMemcpy(d_len, h_lengths, n * 4, hipMemcpyHostToDevice))) &&
+            !(rc = priskv_crc32_ranges_dev(ctx, dptr, d_off, d_len, n, d_crc, nullptr)) &&
+            !(rc = herr(hipDeviceSynchronize())))
+            rc = herr(hipMemcpy(h_out, d_crc, n * 4, hipMemcpyDeviceToHost));
+    }
+    pthread_mutex_unlock(&ctx->lock);
+    if (temp_reg)
+        (void)hipHostUnregister(const_cast<void *>(h_base));
+    return rc;
 }
 
 // ---- host-streamed path ---------------------------------------------------

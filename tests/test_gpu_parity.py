@@ -160,6 +160,58 @@ def test_ranges_vs_oracle(torch_cuda, ctx):
     assert np.array_equal(_u32(out), want)
 
 
+def test_ranges_edges(torch_cuda, ctx):
+    """Extents at every 16-B phase, lengths around 16 / 1 KiB boundaries, ranges
+    starting at byte 0 (rows right-aligned before the region start) and ranges
+    ending exactly at the end of an exactly-sized allocation."""
+    torch = torch_cuda
+    n = 1 << 16
+    t = torch.empty(n, dtype=torch.uint8, device="cuda")  # no padding after the end
+    ctx.fill_splitmix(t, SEED, 7)
+    offs, lens = [], []
+    for off in list(range(0, 34)) + [1000, 4095, 4096, 4097]:
+        for ln in list(range(0, 41)) + [1000, 1023, 1024, 1025, 2047, 2048, 4095, 4096, 4097, 20000]:
+            if off + ln <= n:
+                offs.append(off)
+                lens.append(ln)
+    for ln in (0, 1, 15, 16, 17, 1023, 1024, 1025, 4096, 65535):  # flush with the end
+        offs.append(n - ln)
+        lens.append(ln)
+    offs.append(0)
+    lens.append(n)
+    o = np.array(offs, dtype=np.uint64)
+    ln = np.array(lens, dtype=np.uint32)
+    out = ctx.ranges_dev(t, torch.from_numpy(o.astype(np.int64)).cuda(), torch.from_numpy(ln.view(np.int32)).cuda())
+    torch.cuda.synchronize()
+    assert np.array_equal(_u32(out), O.crc32_ranges(t.cpu().numpy(), o, ln))
+
+
+@pytest.mark.parametrize("register", [False, True])
+def test_ranges_host_scrub(torch_cuda, ctx, register):
+    """Memfile-scrub form: extents of a host region read zero-copy over PCIe."""
+    from priskv_amd import host_register, host_unregister
+    bs = 4096
+    region = O.fill_splitmix(bs * 4096, SEED, 3)  # 16 MiB "value region"
+    rng = np.random.default_rng(8)
+    # values start on block boundaries and span 2^k blocks with a ragged valuelen
+    nval = 1500
+    k = rng.integers(0, 4, nval)
+    blk = rng.integers(0, 4096 - 8, nval)
+    offs = (blk * bs).astype(np.uint64)
+    lens = np.minimum(rng.integers(1, (1 << k) * bs + 1), (4096 - blk) * bs).astype(np.uint32)
+    lens[:4] = [0, 1, 16, bs]
+    if register:
+        host_register(region)
+    try:
+        got = ctx.ranges_host(region, offs, lens)
+    finally:
+        if register:
+            host_unregister(region)
+    assert np.array_equal(got, O.crc32_ranges(region, offs, lens))
+    with pytest.raises(OSError):
+        ctx.ranges_host(region, np.array([region.size - 1], np.uint64), np.array([2], np.uint32))
+
+
 @pytest.mark.parametrize("pinned", [False, True])
 def test_blocks_host_streamed(torch_cuda, ctx, pinned):
     from priskv_amd import host_register, host_unregister

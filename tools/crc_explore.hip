@@ -15,6 +15,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <string>
 #include <vector>
 
 #include "../priskv_amd/csrc/crc_internal.h"
@@ -129,6 +130,13 @@ struct Variant {
                 hipLaunchKernelGGL((crc_rows_kernel<G, CH, NB, AUX, OPT>), g, dim3(kThreads), 0, s, b, n, bs, img, \
                                    fold, o);                                                                   \
             }, {}}
+#define CRC2_VARIANT(G, CH, NB, AUX, WGPC)                                                                     \
+    Variant{"crc2 G" #G " CH" #CH " NBUF" #NB " AUX" #AUX " wg/cu" #WGPC, true, G, CH, WGPC,                \
+            [](dim3 g, hipStream_t s, const uint8_t *b, uint64_t n, uint32_t bs, const uint32_t *img,           \
+               const uint32_t *fold, uint32_t *o) {                                                            \
+                hipLaunchKernelGGL((crc_rows2_kernel<G, CH, NB, AUX>), g, dim3(kThreads), 0, s, b, n / 2, bs, img, \
+                                   fold, o);                                                                   \
+            }, {}}
 #define ROOF_VARIANT(G, CH, NB, AUX, WGPC)                                                                 \
     Variant{"roof G" #G " CH" #CH " NBUF" #NB " AUX" #AUX " wg/cu" #WGPC, false, G, CH, WGPC,             \
             [](dim3 g, hipStream_t s, const uint8_t *b, uint64_t n, uint32_t bs, const uint32_t *img,       \
@@ -169,29 +177,46 @@ int main(int argc, char **argv)
 
     std::vector<Variant> all;
     // first entry = product reference for the bit-exact cross-check and the sustained run
-    all.push_back(CRC_VARIANT(16, 8, 2, 2, 2, 0));
-    all.push_back(CRC_VARIANT(16, 8, 2, 2, 2, 1));
-    all.push_back(CRC_VARIANT(16, 16, 2, 2, 1, 0));
-    all.push_back(CRC_VARIANT(16, 16, 2, 2, 1, 1));
-    all.push_back(CRC_VARIANT(16, 8, 3, 2, 1, 1));
     all.push_back(CRC_VARIANT(32, 8, 2, 2, 1, 0));
-    all.push_back(CRC_VARIANT(32, 8, 2, 2, 1, 1));
-    all.push_back(CRC_VARIANT(32, 8, 2, 2, 2, 1));
-    all.push_back(CRC_VARIANT(32, 4, 3, 2, 2, 1));
-    all.push_back(CRC_VARIANT(32, 16, 2, 2, 1, 1));
+    all.push_back(CRC_VARIANT(32, 8, 2, 2, 1, 2));
+    all.push_back(CRC_VARIANT(32, 8, 2, 2, 1, 3));
+    all.push_back(CRC_VARIANT(16, 16, 2, 2, 1, 0));
+    all.push_back(CRC_VARIANT(16, 16, 2, 2, 1, 2));
+    all.push_back(CRC_VARIANT(16, 16, 2, 2, 1, 3));
+    all.push_back(CRC_VARIANT(32, 8, 2, 2, 2, 2));
     all.push_back(CRC_VARIANT(64, 4, 2, 2, 1, 0));
-    all.push_back(CRC_VARIANT(64, 4, 2, 2, 1, 1));
-    all.push_back(CRC_VARIANT(64, 4, 2, 2, 2, 1));
-    all.push_back(CRC_VARIANT(64, 4, 3, 2, 1, 1));
-    all.push_back(CRC_VARIANT(64, 8, 2, 2, 1, 1));
-    all.push_back(CRC_VARIANT(64, 2, 4, 2, 1, 1));
+    all.push_back(CRC_VARIANT(64, 4, 2, 2, 2, 2));
+    all.push_back(CRC_VARIANT(64, 4, 2, 2, 1, 2));
     all.push_back(ROOF_VARIANT(64, 4, 2, 2, 2));
     all.push_back(ROOF_VARIANT(64, 4, 2, 2, 1));
     all.push_back(ROOF_VARIANT(32, 8, 2, 2, 1));
     all.push_back(ROOF_VARIANT(16, 8, 2, 2, 2));
+    // EXPLORE_FILTER="a,b,c": keep only variants whose name contains one of the substrings
+    std::vector<std::string> filt;
+    if (const char *f = getenv("EXPLORE_FILTER")) {
+        std::string fs(f);
+        size_t p = 0;
+        while (p <= fs.size()) {
+            size_t q = fs.find(',', p);
+            if (q == std::string::npos)
+                q = fs.size();
+            if (q > p)
+                filt.push_back(fs.substr(p, q - p));
+            p = q + 1;
+        }
+    }
+    auto keep = [&](const char *name) {
+        if (filt.empty())
+            return true;
+        for (auto &f : filt)
+            if (strstr(name, f.c_str()))
+                return true;
+        return false;
+    };
     std::vector<Variant> V;
     for (auto &v : all)
-        if (bs % (uint32_t)(v.CH * 16 * v.G) == 0 && nb % (64 / v.G) == 0)
+        if (keep(v.name) && bs % (uint32_t)(v.CH * 16 * v.G) == 0 && nb % (2 * 64 / v.G) == 0 &&
+            (!strstr(v.name, "opt2") && !strstr(v.name, "opt3") || bs == (uint32_t)(v.CH * 16 * v.G)))
             V.push_back(v);
     Variant gs{"roof gridstride nt", false, 64, 1, 8, nullptr, {}};
 

@@ -1,0 +1,8 @@
+set -e
+R=$GRAFT_REPO_ROOT
+O=$R/gpurun_out/r1g
+mkdir -p $O
+timeout -k 10 200 ./tools/crc_explore 4096 $((1<<20)) 4 100 > $O/explore_4k.log 2>&1
+timeout -k 10 200 ./tools/crc_explore 65536 $((1<<16)) 4 100 > $O/explore_64k.log 2>&1
+timeout -k 10 200 ./tools/crc_explore 1048576 4096 4 100 > $O/explore_1m.log 2>&1
+echo ALLDONE
