@@ -231,6 +231,7 @@ def ctx_path(bs, region):
     from priskv_amd import blocks_path
     p = blocks_path(region.data_ptr(), 1, bs)
     if p == "rows":
+        pipe = bs in (1024, 4096)
         if bs <= 16384 and bs % 4096 == 0:
             g, ch = 32, 8
         elif bs <= 16384:
@@ -238,7 +239,7 @@ def ctx_path(bs, region):
         else:
             r = bs // 1024
             g, ch = 64, (4 if r % 4 == 0 else (2 if r % 2 == 0 else 1))
-        return f"crc_rows_kernel<G={g},CH={ch},NBUF=2,nt>"
+        return f"crc_rows_kernel<G={g},CH={ch},NBUF=2,nt{',pipelined-fold' if pipe else ''}>"
     return f"crc_{p}_kernel"
 
 

@@ -144,36 +144,52 @@ int launch_generic(const priskv_crc_ctx *ctx, const uint8_t *base, uint64_t n, u
 constexpr int kNbuf = 2;
 constexpr int kAux = 2;
 
-enum PlanId { PLAN_G32_CH8, PLAN_G16_CH4, PLAN_G64_CH4, PLAN_G64_CH2, PLAN_G64_CH1, NPLANS };
-struct Plan {
-    int G, CH, wg_per_cu;
+enum PlanId {
+    PLAN_G32_CH8_PIPE, // 4 KiB: one chunk == one 2-block group, fold pipelined
+    PLAN_G32_CH8,      // 8 / 12 / 16 KiB
+    PLAN_G16_CH4_PIPE, // 1 KiB
+    PLAN_G16_CH4,      // other multiples of 1 KiB up to 16 KiB
+    PLAN_G64_CH4,      // > 16 KiB
+    PLAN_G64_CH2,
+    PLAN_G64_CH1,
+    NPLANS
 };
-constexpr Plan kPlans[NPLANS] = {{32, 8, 1}, {16, 4, 2}, {64, 4, 1}, {64, 2, 1}, {64, 1, 1}};
+struct Plan {
+    int G, CH, opt, wg_per_cu;
+};
+constexpr Plan kPlans[NPLANS] = {{32, 8, 2, 1}, {32, 8, 0, 1}, {16, 4, 2, 2}, {16, 4, 0, 2},
+                                 {64, 4, 0, 1}, {64, 2, 0, 1}, {64, 1, 0, 1}};
 
 int plan_for(uint32_t bs)
 {
+    if (bs == 4096)
+        return PLAN_G32_CH8_PIPE;
     if (bs <= (16u << 10) && bs % 4096 == 0)
         return PLAN_G32_CH8;
+    if (bs == 1024)
+        return PLAN_G16_CH4_PIPE;
     if (bs <= (16u << 10))
         return PLAN_G16_CH4;
     const uint32_t R = bs / PRV_ROW_BYTES;
     return R % 4 == 0 ? PLAN_G64_CH4 : (R % 2 == 0 ? PLAN_G64_CH2 : PLAN_G64_CH1);
 }
 
-template <int G, int CH>
+template <int G, int CH, int OPT>
 const void *plan_kernel()
 {
-    return reinterpret_cast<const void *>(&crc_rows_kernel<G, CH, kNbuf, kAux>);
+    return reinterpret_cast<const void *>(&crc_rows_kernel<G, CH, kNbuf, kAux, OPT>);
 }
 
 const void *plan_fn(int p)
 {
     switch (p) {
-    case PLAN_G32_CH8: return plan_kernel<32, 8>();
-    case PLAN_G16_CH4: return plan_kernel<16, 4>();
-    case PLAN_G64_CH4: return plan_kernel<64, 4>();
-    case PLAN_G64_CH2: return plan_kernel<64, 2>();
-    default: return plan_kernel<64, 1>();
+    case PLAN_G32_CH8_PIPE: return plan_kernel<32, 8, 2>();
+    case PLAN_G32_CH8: return plan_kernel<32, 8, 0>();
+    case PLAN_G16_CH4_PIPE: return plan_kernel<16, 4, 2>();
+    case PLAN_G16_CH4: return plan_kernel<16, 4, 0>();
+    case PLAN_G64_CH4: return plan_kernel<64, 4, 0>();
+    case PLAN_G64_CH2: return plan_kernel<64, 2, 0>();
+    default: return plan_kernel<64, 1, 0>();
     }
 }
 

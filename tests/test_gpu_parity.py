@@ -186,6 +186,30 @@ def test_ranges_edges(torch_cuda, ctx):
     assert np.array_equal(_u32(out), O.crc32_ranges(t.cpu().numpy(), o, ln))
 
 
+def test_ranges_beyond_2GiB_and_many_per_wave(torch_cuda, ctx):
+    """Extents at offsets with bit 31 (and bit 32) set, and far more extents
+    than waves so each wave loops over many of them (a sign-extension of the
+    low offset half once faulted here)."""
+    torch = torch_cuda
+    n = (5 << 30) + 4096
+    t = torch.empty(n, dtype=torch.uint8, device="cuda")
+    ctx.fill_splitmix(t, SEED, 11)
+    rng = np.random.default_rng(12)
+    k = 40000
+    offs = rng.integers(0, n - 20000, k).astype(np.uint64)
+    offs[:8] = [(1 << 31) - 5, 1 << 31, (1 << 31) + 17, (3 << 30) + 1, 1 << 32, (1 << 32) + 4095,
+                n - 20000, 0]
+    lens = rng.integers(0, 20000, k).astype(np.uint32)
+    out = ctx.ranges_dev(t, torch.from_numpy(offs.astype(np.int64)).cuda(), torch.from_numpy(lens.view(np.int32)).cuda())
+    torch.cuda.synchronize()
+    got = _u32(out)
+    check = list(range(8)) + list(rng.integers(8, k, 300))
+    for i in check:
+        o, ln = int(offs[i]), int(lens[i])
+        assert got[i] == O.crc32(t[o:o + ln].cpu().numpy()), (i, o, ln)
+    del t
+
+
 @pytest.mark.parametrize("register", [False, True])
 def test_ranges_host_scrub(torch_cuda, ctx, register):
     """Memfile-scrub form: extents of a host region read zero-copy over PCIe."""

@@ -1,0 +1,148 @@
+#!/usr/bin/env python3
+"""Throughput of every API path of libpriskv_crc.so on one GPU.
+
+Not the driver's benchmark (that is bench.py); this times the secondary
+paths -- every block-size plan including sub-KiB and generic sizes, the
+per-value extent kernel on device and host (zero-copy scrub), and the
+host-streamed block path -- each checked against the CPU oracle on a sample.
+One JSON line per case on stdout.
+"""
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+import _oracle as O  # noqa: E402
+import torch  # noqa: E402
+
+from priskv_amd import CrcContext, as_u32, blocks_path, host_register, host_unregister  # noqa: E402
+
+SEED = 0x5EED5EED
+
+
+def timeit(fn, steps, warm_s=0.2):
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < warm_s:
+        fn()
+        torch.cuda.synchronize()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ev0.record()
+    for _ in range(steps):
+        fn()
+    ev1.record()
+    torch.cuda.synchronize()
+    return ev0.elapsed_time(ev1) / steps * 1e-3
+
+
+def emit(**kw):
+    print(json.dumps(kw), flush=True)
+
+
+def blocks_case(ctx, bs, total, steps=10):
+    nb = total // bs
+    t = torch.empty(nb * bs, dtype=torch.uint8, device="cuda")
+    ctx.fill_splitmix(t, SEED ^ bs, 0)
+    out = torch.empty(nb, dtype=torch.int32, device="cuda")
+    sec = timeit(lambda: ctx.blocks_dev(t, bs, out=out), steps)
+    samp = min(nb, max(1, (256 << 20) // bs))
+    ok = np.array_equal(as_u32(out[:samp]), O.crc32_blocks(t[: samp * bs].cpu().numpy(), bs, nthreads=16))
+    emit(path="blocks_dev", kernel=blocks_path(t.data_ptr(), nb, bs), block_size=bs, nblocks=nb,
+         ms=round(sec * 1e3, 4), GiBs=round(nb * bs / sec / 2**30, 1), TBs=round(nb * (bs + 4) / sec / 1e12, 3),
+         checked=samp, bit_exact=bool(ok))
+    del t, out
+
+
+def extents(rng, n, region_bytes, bs):
+    """Values as PrisKV stores them: start on a block, occupy 2^k blocks,
+    valuelen ragged inside the last block (server/buddy.c:134-140)."""
+    k = rng.integers(0, 3, n)
+    span = (1 << k) * bs
+    blk = rng.integers(0, region_bytes // bs - 4, n)
+    offs = (blk * bs).astype(np.uint64)
+    lens = np.minimum(span - rng.integers(0, bs, n), region_bytes - offs).astype(np.uint32)
+    return offs, lens
+
+
+def ranges_dev_case(ctx, bs=4096, region=4 << 30, n=1 << 19, steps=10):
+    rng = np.random.default_rng(1)
+    t = torch.empty(region, dtype=torch.uint8, device="cuda")
+    ctx.fill_splitmix(t, SEED, 0)
+    offs, lens = extents(rng, n, region, bs)
+    d_o = torch.from_numpy(offs.astype(np.int64)).cuda()
+    d_l = torch.from_numpy(lens.view(np.int32)).cuda()
+    out = torch.empty(n, dtype=torch.int32, device="cuda")
+    sec = timeit(lambda: ctx.ranges_dev(t, d_o, d_l, out=out), steps)
+    samp = 20000
+    host = None
+    got = as_u32(out[:samp])
+    want = np.array([O.crc32(t[int(o):int(o) + int(ln)].cpu().numpy()) for o, ln in zip(offs[:200], lens[:200])],
+                    dtype=np.uint32)
+    ok = np.array_equal(got[:200], want)
+    vb = int(lens.astype(np.uint64).sum())
+    emit(path="ranges_dev", values=n, value_bytes=vb, mean_len=round(vb / n), ms=round(sec * 1e3, 4),
+         GiBs=round(vb / sec / 2**30, 1), checked=200, bit_exact=bool(ok))
+    del t, host
+
+
+def ranges_host_case(ctx, bs=4096, region=2 << 30, n=1 << 17):
+    rng = np.random.default_rng(2)
+    host = O.fill_splitmix(region, SEED, 0)
+    offs, lens = extents(rng, n, region, bs)
+    host_register(host)
+    try:
+        ctx.ranges_host(host, offs, lens)
+        t0 = time.perf_counter()
+        reps = 3
+        for _ in range(reps):
+            got = ctx.ranges_host(host, offs, lens)
+        sec = (time.perf_counter() - t0) / reps
+    finally:
+        host_unregister(host)
+    ok = np.array_equal(got[:5000], O.crc32_ranges(host, offs[:5000], lens[:5000]))
+    vb = int(lens.astype(np.uint64).sum())
+    emit(path="ranges_host_zero_copy", values=n, value_bytes=vb, ms=round(sec * 1e3, 2),
+         GiBs=round(vb / sec / 2**30, 2), checked=5000, bit_exact=bool(ok))
+
+
+def blocks_host_case(ctx, bs=4096, total=2 << 30):
+    host = O.fill_splitmix(total, SEED, 0)
+    res = {}
+    for mode in ("registered", "pageable"):
+        if mode == "registered":
+            host_register(host)
+        ctx.blocks_host(host, bs)
+        t0 = time.perf_counter()
+        for _ in range(3):
+            got = ctx.blocks_host(host, bs)
+        res[mode] = total / ((time.perf_counter() - t0) / 3) / 2**30
+        if mode == "registered":
+            host_unregister(host)
+    ok = np.array_equal(got[:65536], O.crc32_blocks(host[: 65536 * bs], bs, nthreads=16))
+    emit(path="blocks_host_streamed", block_size=bs, bytes=total, registered_GiBs=round(res["registered"], 2),
+         pageable_GiBs=round(res["pageable"], 2), checked=65536, bit_exact=bool(ok))
+
+
+def main():
+    which = sys.argv[1:] or ["blocks", "ranges", "host"]
+    ctx = CrcContext(0)
+    if "blocks" in which:
+        for bs in (16, 64, 256, 512, 1024, 2048, 3072, 4096, 8192, 16384, 20480, 65536, 1 << 20, 100, 4100):
+            total = (1 << 30) if bs >= 1024 else (256 << 20)
+            if bs in (100, 4100):
+                total = 64 << 20
+            blocks_case(ctx, bs, total)
+    if "ranges" in which:
+        ranges_dev_case(ctx)
+    if "host" in which:
+        ranges_host_case(ctx)
+        blocks_host_case(ctx)
+
+
+if __name__ == "__main__":
+    main()
