@@ -178,3 +178,14 @@ def test_ctx_create_without_gpu_is_enodev():
         pytest.skip("GPU present")
     h = ctypes.c_void_p()
     assert C.lib().priskv_crc_ctx_create(0, ctypes.byref(h)) == -19
+
+
+def test_library_is_not_stale():
+    """The shipped .so must be newer than every source it is built from (a
+    stale build once sent an already-fixed kernel bug to the GPU box)."""
+    csrc = os.path.join(ROOT, "priskv_amd", "csrc")
+    srcs = [os.path.join(csrc, f) for f in os.listdir(csrc) if f.endswith((".hip", ".inc", ".c", ".h"))]
+    srcs += [os.path.join(INCLUDE, f) for f in os.listdir(INCLUDE)]
+    newest = max(os.path.getmtime(p) for p in srcs)
+    for lib in ("libpriskv_crc.so", "libpriskv_crc_host.a"):
+        assert os.path.getmtime(os.path.join(LIBDIR, lib)) >= newest, f"{lib} older than its sources: run make"
