@@ -181,11 +181,14 @@ def test_ctx_create_without_gpu_is_enodev():
 
 
 def test_library_is_not_stale():
-    """The shipped .so must be newer than every source it is built from (a
+    """Each shipped library must be newer than every source it is built from (a
     stale build once sent an already-fixed kernel bug to the GPU box)."""
     csrc = os.path.join(ROOT, "priskv_amd", "csrc")
-    srcs = [os.path.join(csrc, f) for f in os.listdir(csrc) if f.endswith((".hip", ".inc", ".c", ".h"))]
-    srcs += [os.path.join(INCLUDE, f) for f in os.listdir(INCLUDE)]
-    newest = max(os.path.getmtime(p) for p in srcs)
-    for lib in ("libpriskv_crc.so", "libpriskv_crc_host.a"):
+    headers = [os.path.join(INCLUDE, f) for f in os.listdir(INCLUDE)] + [os.path.join(csrc, "crc_internal.h")]
+    deps = {
+        "libpriskv_crc.so": headers + [os.path.join(csrc, f) for f in ("crc_gpu.hip", "crc_device.inc", "crc_host.c")],
+        "libpriskv_crc_host.a": headers + [os.path.join(csrc, "crc_host.c")],
+    }
+    for lib, srcs in deps.items():
+        newest = max(os.path.getmtime(p) for p in srcs)
         assert os.path.getmtime(os.path.join(LIBDIR, lib)) >= newest, f"{lib} older than its sources: run make"
