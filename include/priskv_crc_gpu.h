@@ -108,8 +108,10 @@ int priskv_crc_fill_splitmix_dev(const priskv_crc_ctx *ctx, void *d_dst, uint64_
 
 /* Which kernel a (d_base, block_size) batch dispatches to: 1 = rows (block
  * a multiple of 1 KiB, 16-byte aligned base: G = 16/32/64 lanes per block),
- * 3 = sub-KiB power-of-two blocks, 4 = generic (any size / alignment); 2 is
- * reserved.  For tests and benchmarks; -EINVAL for invalid arguments. */
+ * 2 = extents (any other block >= 1 KiB or any base alignment: one wave per
+ * block, masked rows + byte-serial tail), 3 = sub-KiB power-of-two blocks,
+ * 4 = generic (smaller odd sizes: one thread per block).  For tests and
+ * benchmarks; -EINVAL for invalid arguments. */
 int priskv_crc32_blocks_path(const void *d_base, uint64_t nblocks, uint32_t block_size);
 
 const char *priskv_crc_version(void);

@@ -104,7 +104,7 @@ inline int herr(hipError_t e)
 
 inline bool is_pow2(uint64_t v) { return v && !(v & (v - 1)); }
 
-enum Path { PATH_ROWS = 1, PATH_ROWS_COOP = 2, PATH_SMALL = 3, PATH_GENERIC = 4 };
+enum Path { PATH_ROWS = 1, PATH_EXTENTS = 2, PATH_SMALL = 3, PATH_GENERIC = 4 };
 
 int choose_path(const void *d_base, uint32_t block_size)
 {
@@ -113,6 +113,8 @@ int choose_path(const void *d_base, uint32_t block_size)
         return PATH_ROWS;
     if (aligned && is_pow2(block_size) && block_size >= 16 && block_size <= 512)
         return PATH_SMALL;
+    if (block_size >= PRV_ROW_BYTES)
+        return PATH_EXTENTS;
     return PATH_GENERIC;
 }
 
@@ -134,6 +136,20 @@ int launch_generic(const priskv_crc_ctx *ctx, const uint8_t *base, uint64_t n, u
         grid = 1;
     hipLaunchKernelGGL(crc_generic_kernel, dim3(grid), dim3(256), 0, s, base, n, stride, len_const, offs,
                        lens, ctx->d_sarwate, out);
+    return herr(hipGetLastError());
+}
+
+// extents through the row machinery (any base alignment, any lengths)
+int launch_extents(const priskv_crc_ctx *ctx, const uint8_t *base, uint64_t n, const uint64_t *offs,
+                   const uint32_t *lens, uint64_t stride, uint32_t len_const, uint32_t *out, hipStream_t s)
+{
+    const uint64_t shift = (uintptr_t)base & 15;
+    const uint8_t *abase = base - shift;
+    const uint64_t want = (n + kWaves - 1) / kWaves;
+    const uint64_t cap = (uint64_t)ctx->num_cus * 2;
+    const uint32_t grid = (uint32_t)(want < cap ? want : cap);
+    hipLaunchKernelGGL(crc_ranges_kernel, dim3(grid), dim3(kThreads), 0, s, abase, n, offs, lens, shift, stride,
+                       len_const, ctx->d_lds_image[0], ctx->d_fold + 6 * 2048, ctx->d_sarwate, out);
     return herr(hipGetLastError());
 }
 
@@ -260,6 +276,8 @@ int launch_blocks(const priskv_crc_ctx *ctx, const uint8_t *base, uint64_t nbloc
         }
         return herr(hipGetLastError());
     }
+    if (bs >= PRV_ROW_BYTES)
+        return launch_extents(ctx, base, nblocks, nullptr, nullptr, bs, bs, out, s);
     return launch_generic(ctx, base, nblocks, bs, bs, nullptr, nullptr, out, s);
 }
 
@@ -398,18 +416,7 @@ int priskv_crc32_ranges_dev(const priskv_crc_ctx *ctx, const void *d_base, const
     DevGuard g(ctx->device);
     if (!g.ok)
         return -ENODEV;
-    // one wave per extent; the base must be 16-B aligned for the row path
-    // (device allocations are), otherwise the byte-serial generic kernel
-    if ((uintptr_t)d_base & 15)
-        return launch_generic(ctx, (const uint8_t *)d_base, n, 0, 0, d_offsets, d_lengths, d_out,
-                              (hipStream_t)stream);
-    const uint64_t want = (n + kWaves - 1) / kWaves;
-    const uint64_t cap = (uint64_t)ctx->num_cus * 2;
-    const uint32_t grid = (uint32_t)(want < cap ? want : cap);
-    hipLaunchKernelGGL(crc_ranges_kernel, dim3(grid), dim3(kThreads), 0, (hipStream_t)stream,
-                       (const uint8_t *)d_base, n, d_offsets, d_lengths, ctx->d_lds_image[0], ctx->d_fold + 6 * 2048,
-                       ctx->d_sarwate, d_out);
-    return herr(hipGetLastError());
+    return launch_extents(ctx, (const uint8_t *)d_base, n, d_offsets, d_lengths, 0, 0, d_out, (hipStream_t)stream);
 }
 
 int priskv_crc_fill_splitmix_dev(const priskv_crc_ctx *ctx, void *d_dst, uint64_t nbytes, uint64_t seed,

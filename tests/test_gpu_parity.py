@@ -79,9 +79,10 @@ def test_golden_ranges_on_gpu(torch_cuda, ctx, golden):
 # (priskv_amd/csrc/crc_gpu.hip plan_for):
 #   G32/CH8 (4K, 8K, 12K, 16K), G16/CH4 (1K, 2K, 3K, 5K, 6K),
 #   G64/CH4 (20K, 64K, 1M), G64/CH2 (18K), G64/CH1 (17K, 33K),
-#   sub-KiB (16..512), generic (odd sizes / 16-B multiples that are not powers of two)
+#   sub-KiB (16..512), extents (>= 1 KiB not a multiple of 1 KiB), generic (smaller odd sizes)
 BLOCK_SIZES = [1024, 2048, 3072, 4096, 5120, 6144, 8192, 12288, 16384, 17408, 18432, 20480, 33792,
-               65536, 1 << 20, 16, 32, 64, 128, 256, 512, 1, 3, 100, 1000, 4097, 4100, 48]
+               65536, 1 << 20, 16, 32, 64, 128, 256, 512, 1, 3, 100, 1000, 4097, 4100, 48, 1025, 1040,
+               65537, 70000]
 NBLOCKS = [1, 2, 7, 63, 64, 65, 129, 1000, 4099]
 
 
@@ -100,10 +101,11 @@ def test_blocks_vs_oracle(torch_cuda, ctx, bs):
         assert np.array_equal(got, want), (bs, nb, np.nonzero(got != want)[0][:8])
 
 
-@pytest.mark.parametrize("misalign", [1, 2, 4, 8, 12])
-def test_unaligned_base(torch_cuda, ctx, misalign):
+@pytest.mark.parametrize("misalign", [1, 2, 4, 8, 12, 15])
+@pytest.mark.parametrize("bs", [4096, 1000, 4100])
+def test_unaligned_base(torch_cuda, ctx, misalign, bs):
     torch = torch_cuda
-    bs, nb = 4096, 97
+    nb = 97
     t = _region(torch, ctx, bs * nb + 64, SEED, 3)
     view = t[misalign: misalign + bs * nb]
     out = ctx.blocks_dev(view, bs, nblocks=nb)
@@ -169,6 +171,7 @@ def test_ranges_edges(torch_cuda, ctx):
     t = torch.empty(n, dtype=torch.uint8, device="cuda")  # no padding after the end
     ctx.fill_splitmix(t, SEED, 7)
     offs, lens = [], []
+    # (also run below through an unaligned view of the same bytes)
     for off in list(range(0, 34)) + [1000, 4095, 4096, 4097]:
         for ln in list(range(0, 41)) + [1000, 1023, 1024, 1025, 2047, 2048, 4095, 4096, 4097, 20000]:
             if off + ln <= n:
@@ -184,6 +187,14 @@ def test_ranges_edges(torch_cuda, ctx):
     out = ctx.ranges_dev(t, torch.from_numpy(o.astype(np.int64)).cuda(), torch.from_numpy(ln.view(np.int32)).cuda())
     torch.cuda.synchronize()
     assert np.array_equal(_u32(out), O.crc32_ranges(t.cpu().numpy(), o, ln))
+    # unaligned region base: the same extents relative to base + 5 (re-based in the library)
+    keep = (o + ln.astype(np.uint64)) <= n - 5
+    o2, l2 = o[keep], ln[keep]
+    view = t[5:]
+    out2 = ctx.ranges_dev(view, torch.from_numpy(o2.astype(np.int64)).cuda(),
+                          torch.from_numpy(l2.view(np.int32)).cuda())
+    torch.cuda.synchronize()
+    assert np.array_equal(_u32(out2), O.crc32_ranges(view.cpu().numpy(), o2, l2))
 
 
 def test_ranges_beyond_2GiB_and_many_per_wave(torch_cuda, ctx):

@@ -168,8 +168,11 @@ def test_path_selection():
     assert C.blocks_path(4096, 10, 256) == "small"
     assert C.blocks_path(4096, 10, 16) == "small"
     assert C.blocks_path(4096, 10, 100) == "generic"
-    assert C.blocks_path(4097, 10, 4096) == "generic"   # unaligned base
-    assert C.blocks_path(4104, 10, 4096) == "generic"   # 8-byte aligned only
+    assert C.blocks_path(4097, 10, 100) == "generic"
+    assert C.blocks_path(4097, 10, 4096) == "extents"   # unaligned base
+    assert C.blocks_path(4104, 10, 4096) == "extents"   # 8-byte aligned only
+    assert C.blocks_path(4096, 10, 4100) == "extents"   # not a multiple of 1 KiB
+    assert C.blocks_path(4096, 10, 1000) == "generic"
 
 
 def test_ctx_create_without_gpu_is_enodev():
