@@ -88,8 +88,21 @@ int priskv_crc32_ranges_host(priskv_crc_ctx *ctx, const void *h_base, uint64_t r
 int priskv_crc32_blocks_host(priskv_crc_ctx *ctx, const void *h_base, uint64_t nblocks,
                              uint32_t block_size, uint32_t *h_out);
 
+/* Multi-GPU form of the two host-resident entry points: the blocks (or the
+ * extents) are split into nctx contiguous shards, shard g = [g*n/nctx,
+ * (g+1)*n/nctx), and each context's device works on its own shard from its
+ * own host thread -- each GPU pulls over its own PCIe link, no collective.
+ * Returns the first shard's error, if any.  Contexts must be distinct
+ * objects (they may share a device). */
+int priskv_crc32_blocks_host_multi(priskv_crc_ctx *const *ctxs, int nctx, const void *h_base,
+                                   uint64_t nblocks, uint32_t block_size, uint32_t *h_out);
+int priskv_crc32_ranges_host_multi(priskv_crc_ctx *const *ctxs, int nctx, const void *h_base,
+                                   uint64_t region_bytes, const uint64_t *h_offsets,
+                                   const uint32_t *h_lengths, uint64_t n, uint32_t *h_out);
+
 /* Page-lock an existing host range (e.g. the mmap'd memfile value region,
- * server/memory.c:351-457) for direct DMA, and undo it. */
+ * server/memory.c:351-457) for direct DMA and zero-copy reads by every GPU
+ * (portable + mapped), and undo it. */
 int priskv_crc_host_register(void *h_base, uint64_t len);
 int priskv_crc_host_unregister(void *h_base);
 

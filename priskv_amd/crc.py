@@ -45,6 +45,10 @@ SIGNATURES = [
      [_C.c_void_p, _C.c_void_p, _C.c_uint64, _C.c_uint32, _C.c_void_p]),
     ("priskv_crc32_ranges_host", _C.c_int,
      [_C.c_void_p, _C.c_void_p, _C.c_uint64, _C.c_void_p, _C.c_void_p, _C.c_uint64, _C.c_void_p]),
+    ("priskv_crc32_blocks_host_multi", _C.c_int,
+     [_C.c_void_p, _C.c_int, _C.c_void_p, _C.c_uint64, _C.c_uint32, _C.c_void_p]),
+    ("priskv_crc32_ranges_host_multi", _C.c_int,
+     [_C.c_void_p, _C.c_int, _C.c_void_p, _C.c_uint64, _C.c_void_p, _C.c_void_p, _C.c_uint64, _C.c_void_p]),
     ("priskv_crc_host_register", _C.c_int, [_C.c_void_p, _C.c_uint64]),
     ("priskv_crc_host_unregister", _C.c_int, [_C.c_void_p]),
     ("priskv_crc32_shift", _C.c_uint32, [_C.c_uint32, _C.c_uint64]),
@@ -217,6 +221,35 @@ def _ranges_host(self, region: np.ndarray, offsets, lengths, out: Optional[np.nd
 
 
 CrcContext.ranges_host = _ranges_host
+
+
+def _ctx_array(ctxs):
+    arr = (ctypes.c_void_p * len(ctxs))(*[c.handle.value for c in ctxs])
+    return arr
+
+
+def blocks_host_multi(ctxs, region: np.ndarray, block_size: int, out: Optional[np.ndarray] = None) -> np.ndarray:
+    """Host-resident blocks split across several contexts (one GPU each)."""
+    region = np.ascontiguousarray(region).view(np.uint8).reshape(-1)
+    n = region.size // block_size
+    if out is None:
+        out = np.empty(n, dtype=np.uint32)
+    _check(lib().priskv_crc32_blocks_host_multi(_ctx_array(ctxs), len(ctxs), region.ctypes.data, n, block_size,
+                                                out.ctypes.data), "priskv_crc32_blocks_host_multi")
+    return out
+
+
+def ranges_host_multi(ctxs, region: np.ndarray, offsets, lengths, out: Optional[np.ndarray] = None) -> np.ndarray:
+    """Host extents (memfile scrub) split across several contexts (one GPU each)."""
+    region = np.ascontiguousarray(region).view(np.uint8).reshape(-1)
+    offs = np.ascontiguousarray(offsets, dtype=np.uint64)
+    lens = np.ascontiguousarray(lengths, dtype=np.uint32)
+    if out is None:
+        out = np.empty(offs.size, dtype=np.uint32)
+    _check(lib().priskv_crc32_ranges_host_multi(_ctx_array(ctxs), len(ctxs), region.ctypes.data, region.size,
+                                                offs.ctypes.data, lens.ctypes.data, offs.size, out.ctypes.data),
+           "priskv_crc32_ranges_host_multi")
+    return out
 
 
 def as_u32(t) -> np.ndarray:

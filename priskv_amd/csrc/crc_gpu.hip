@@ -71,6 +71,7 @@ struct priskv_crc_ctx {
     // host-extent scrub scratch (guarded by lock)
     size_t scrub_cap;
     void *d_scrub; // offsets | lengths | crcs
+    hipStream_t aux; // the context's own stream for synchronous host-resident calls
 };
 
 namespace {
@@ -352,6 +353,8 @@ int priskv_crc_ctx_create(int device, priskv_crc_ctx **out)
     }
     if ((rc = rows_occupancy(c)))
         goto fail;
+    if ((rc = herr(hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking))))
+        goto fail;
     free(h_img);
     free(h_fold);
     *out = c;
@@ -383,6 +386,8 @@ void priskv_crc_ctx_destroy(priskv_crc_ctx *c)
     (void)hipFree(c->d_fold);
     (void)hipFree(c->d_sarwate);
     (void)hipFree(c->d_scrub);
+    if (c->aux)
+        (void)hipStreamDestroy(c->aux);
     pthread_mutex_destroy(&c->lock);
     free(c);
 }
@@ -443,7 +448,7 @@ int priskv_crc_host_register(void *h_base, uint64_t len)
 {
     if (!h_base || !len)
         return -EINVAL;
-    return herr(hipHostRegister(h_base, len, hipHostRegisterDefault));
+    return herr(hipHostRegister(h_base, len, hipHostRegisterPortable | hipHostRegisterMapped));
 }
 
 int priskv_crc_host_unregister(void *h_base)
@@ -475,7 +480,8 @@ int priskv_crc32_ranges_host(priskv_crc_ctx *ctx, const void *h_base, uint64_t r
     bool temp_reg = false;
     if (hipHostGetDevicePointer(&dptr, const_cast<void *>(h_base), 0) != hipSuccess || !dptr) {
         (void)hipGetLastError();
-        if (int rc = herr(hipHostRegister(const_cast<void *>(h_base), region_bytes, hipHostRegisterMapped)))
+        if (int rc = herr(hipHostRegister(const_cast<void *>(h_base), region_bytes,
+                                          hipHostRegisterPortable | hipHostRegisterMapped)))
             return rc;
         temp_reg = true;
         if (int rc = herr(hipHostGetDevicePointer(&dptr, const_cast<void *>(h_base), 0))) {
@@ -497,13 +503,126 @@ int priskv_crc32_ranges_host(priskv_crc_ctx *ctx, const void *h_base, uint64_t r
         uint64_t *d_off = (uint64_t *)ctx->d_scrub;
         uint32_t *d_len = (uint32_t *)(d_off + n);
         uint32_t *d_crc = d_len + n;
-        if (!(rc = herr(hipMemcpy(d_off, h_offsets, n * 8, hipMemcpyHostToDevice))) &&
-            !(rc = herr(hipMemcpy(d_len, h_lengths, n * 4, hipMemcpyHostToDevice))) &&
-            !(rc = priskv_crc32_ranges_dev(ctx, dptr, d_off, d_len, n, d_crc, nullptr)) &&
-            !(rc = herr(hipDeviceSynchronize())))
-            rc = herr(hipMemcpy(h_out, d_crc, n * 4, hipMemcpyDeviceToHost));
+        if (!(rc = herr(hipMemcpyAsync(d_off, h_offsets, n * 8, hipMemcpyHostToDevice, ctx->aux))) &&
+            !(rc = herr(hipMemcpyAsync(d_len, h_lengths, n * 4, hipMemcpyHostToDevice, ctx->aux))) &&
+            !(rc = priskv_crc32_ranges_dev(ctx, dptr, d_off, d_len, n, d_crc, ctx->aux)) &&
+            !(rc = herr(hipMemcpyAsync(h_out, d_crc, n * 4, hipMemcpyDeviceToHost, ctx->aux))))
+            rc = herr(hipStreamSynchronize(ctx->aux));
+        else
+            (void)hipStreamSynchronize(ctx->aux);
     }
     pthread_mutex_unlock(&ctx->lock);
+    if (temp_reg)
+        (void)hipHostUnregister(const_cast<void *>(h_base));
+    return rc;
+}
+
+// ---- multi-GPU host-resident forms ------------------------------------------
+struct MultiJob {
+    priskv_crc_ctx *ctx;
+    const void *base;
+    uint64_t region_bytes;
+    const uint64_t *offs;
+    const uint32_t *lens;
+    uint64_t first, n;
+    uint32_t bs;
+    uint32_t *out;
+    bool ranges;
+    int rc;
+};
+
+static void *multi_worker(void *arg)
+{
+    MultiJob *j = (MultiJob *)arg;
+    if (!j->n) {
+        j->rc = 0;
+    } else if (j->ranges) {
+        j->rc = priskv_crc32_ranges_host(j->ctx, j->base, j->region_bytes, j->offs + j->first, j->lens + j->first,
+                                         j->n, j->out + j->first);
+    } else {
+        j->rc = priskv_crc32_blocks_host(j->ctx, (const uint8_t *)j->base + j->first * (uint64_t)j->bs, j->n,
+                                         j->bs, j->out + j->first);
+    }
+    return nullptr;
+}
+
+static int run_multi(priskv_crc_ctx *const *ctxs, int nctx, MultiJob proto, uint64_t n)
+{
+    if (!ctxs || nctx < 1 || nctx > 64)
+        return -EINVAL;
+    for (int g = 0; g < nctx; g++)
+        for (int h = 0; h < g; h++)
+            if (!ctxs[g] || ctxs[g] == ctxs[h])
+                return -EINVAL;
+    if (!ctxs[0])
+        return -EINVAL;
+    MultiJob jobs[64];
+    pthread_t th[64];
+    for (int g = 0; g < nctx; g++) {
+        jobs[g] = proto;
+        jobs[g].ctx = ctxs[g];
+        jobs[g].first = n * (uint64_t)g / (uint64_t)nctx;
+        jobs[g].n = n * (uint64_t)(g + 1) / (uint64_t)nctx - jobs[g].first;
+        jobs[g].rc = -EIO;
+    }
+    int started = 1;
+    for (int g = 1; g < nctx; g++, started++)
+        if (pthread_create(&th[g], nullptr, multi_worker, &jobs[g]))
+            break;
+    multi_worker(&jobs[0]);
+    for (int g = 1; g < started; g++)
+        pthread_join(th[g], nullptr);
+    for (int g = started; g < nctx; g++) // threads that could not start: run inline
+        multi_worker(&jobs[g]);
+    for (int g = 0; g < nctx; g++)
+        if (jobs[g].rc)
+            return jobs[g].rc;
+    return 0;
+}
+
+int priskv_crc32_blocks_host_multi(priskv_crc_ctx *const *ctxs, int nctx, const void *h_base, uint64_t nblocks,
+                                   uint32_t block_size, uint32_t *h_out)
+{
+    if (block_size == 0)
+        return -EINVAL;
+    if (nblocks == 0)
+        return (ctxs && nctx >= 1) ? 0 : -EINVAL;
+    if (!h_base || !h_out)
+        return -EINVAL;
+    MultiJob p{};
+    p.base = h_base;
+    p.bs = block_size;
+    p.out = h_out;
+    p.ranges = false;
+    return run_multi(ctxs, nctx, p, nblocks);
+}
+
+int priskv_crc32_ranges_host_multi(priskv_crc_ctx *const *ctxs, int nctx, const void *h_base, uint64_t region_bytes,
+                                   const uint64_t *h_offsets, const uint32_t *h_lengths, uint64_t n, uint32_t *h_out)
+{
+    if (n == 0)
+        return (ctxs && nctx >= 1) ? 0 : -EINVAL;
+    if (!h_base || !h_offsets || !h_lengths || !h_out || !region_bytes)
+        return -EINVAL;
+    MultiJob p{};
+    p.base = h_base;
+    p.region_bytes = region_bytes;
+    p.offs = h_offsets;
+    p.lens = h_lengths;
+    p.out = h_out;
+    p.ranges = true;
+    // register the mapping once for all devices (the per-shard calls would
+    // otherwise race to register the same range)
+    void *probe = nullptr;
+    bool temp_reg = false;
+    if (hipHostGetDevicePointer(&probe, const_cast<void *>(h_base), 0) != hipSuccess || !probe) {
+        (void)hipGetLastError();
+        if (int rc = herr(hipHostRegister(const_cast<void *>(h_base), region_bytes,
+                                          hipHostRegisterPortable | hipHostRegisterMapped)))
+            return rc;
+        temp_reg = true;
+    }
+    const int rc = run_multi(ctxs, nctx, p, n);
     if (temp_reg)
         (void)hipHostUnregister(const_cast<void *>(h_base));
     return rc;

@@ -247,6 +247,38 @@ def test_ranges_host_scrub(torch_cuda, ctx, register):
         ctx.ranges_host(region, np.array([region.size - 1], np.uint64), np.array([2], np.uint32))
 
 
+def test_multi_gpu_host_paths(torch_cuda, ctx):
+    """Multi-GPU host-resident forms with 2-3 contexts (all on the visible
+    device(s); on the 8-GPU node each context is its own GPU)."""
+    from priskv_amd import CrcContext, blocks_host_multi, host_register, host_unregister, ranges_host_multi
+    ndev = torch_cuda.cuda.device_count()
+    ctxs = [CrcContext(i % ndev) for i in range(3)]
+    try:
+        bs = 4096
+        host = O.fill_splitmix(bs * 20011, SEED, 9)
+        want = O.crc32_blocks(host, bs, nthreads=8)
+        assert np.array_equal(blocks_host_multi(ctxs, host, bs), want)
+        host_register(host)
+        try:
+            assert np.array_equal(blocks_host_multi(ctxs[:2], host, bs), want)
+            rng = np.random.default_rng(3)
+            offs = (rng.integers(0, 20000, 5000) * bs).astype(np.uint64)
+            lens = rng.integers(0, 3 * bs, 5000).astype(np.uint32)
+            lens = np.minimum(lens, (host.size - offs)).astype(np.uint32)
+            assert np.array_equal(ranges_host_multi(ctxs, host, offs, lens), O.crc32_ranges(host, offs, lens))
+        finally:
+            host_unregister(host)
+        # unregistered region: registered once for all devices inside the call
+        offs = np.array([0, 4096, 123], np.uint64)
+        lens = np.array([4096, 100, 5000], np.uint32)
+        assert np.array_equal(ranges_host_multi(ctxs[:2], host, offs, lens), O.crc32_ranges(host, offs, lens))
+        with pytest.raises(OSError):
+            blocks_host_multi([ctxs[0], ctxs[0]], host, bs)  # same context twice
+    finally:
+        for c in ctxs:
+            c.close()
+
+
 @pytest.mark.parametrize("pinned", [False, True])
 def test_blocks_host_streamed(torch_cuda, ctx, pinned):
     from priskv_amd import host_register, host_unregister

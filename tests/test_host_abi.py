@@ -159,6 +159,13 @@ def test_batch_entry_points_reject_bad_args_without_gpu():
     assert L.priskv_crc_fill_splitmix_dev(None, 16, 16, 0, 0, None) == -22
     assert L.priskv_crc32_blocks_path(None, 1, 4096) == -22
     assert L.priskv_crc32_blocks_path(16, 1, 0) == -22
+    assert L.priskv_crc32_ranges_host(None, 1, 16, 1, 1, 1, 1) == -22
+    # multi-GPU forms: no contexts, zero contexts, NULL context entries
+    null2 = (ctypes.c_void_p * 2)(None, None)
+    assert L.priskv_crc32_blocks_host_multi(None, 1, 16, 1, 4096, 16) == -22
+    assert L.priskv_crc32_blocks_host_multi(null2, 0, 16, 1, 4096, 16) == -22
+    assert L.priskv_crc32_blocks_host_multi(null2, 2, 16, 1, 4096, 16) == -22
+    assert L.priskv_crc32_ranges_host_multi(null2, 2, 16, 64, 16, 16, 1, 16) == -22
 
 
 def test_path_selection():
