@@ -546,15 +546,23 @@ static void *multi_worker(void *arg)
     return nullptr;
 }
 
-static int run_multi(priskv_crc_ctx *const *ctxs, int nctx, MultiJob proto, uint64_t n)
+static bool valid_ctxs(priskv_crc_ctx *const *ctxs, int nctx)
 {
     if (!ctxs || nctx < 1 || nctx > 64)
-        return -EINVAL;
-    for (int g = 0; g < nctx; g++)
+        return false;
+    for (int g = 0; g < nctx; g++) {
+        if (!ctxs[g])
+            return false;
         for (int h = 0; h < g; h++)
-            if (!ctxs[g] || ctxs[g] == ctxs[h])
-                return -EINVAL;
-    if (!ctxs[0])
+            if (ctxs[g] == ctxs[h])
+                return false;
+    }
+    return true;
+}
+
+static int run_multi(priskv_crc_ctx *const *ctxs, int nctx, MultiJob proto, uint64_t n)
+{
+    if (!valid_ctxs(ctxs, nctx))
         return -EINVAL;
     MultiJob jobs[64];
     pthread_t th[64];
@@ -583,10 +591,10 @@ static int run_multi(priskv_crc_ctx *const *ctxs, int nctx, MultiJob proto, uint
 int priskv_crc32_blocks_host_multi(priskv_crc_ctx *const *ctxs, int nctx, const void *h_base, uint64_t nblocks,
                                    uint32_t block_size, uint32_t *h_out)
 {
-    if (block_size == 0)
+    if (block_size == 0 || !valid_ctxs(ctxs, nctx))
         return -EINVAL;
     if (nblocks == 0)
-        return (ctxs && nctx >= 1) ? 0 : -EINVAL;
+        return 0;
     if (!h_base || !h_out)
         return -EINVAL;
     MultiJob p{};
@@ -600,10 +608,18 @@ int priskv_crc32_blocks_host_multi(priskv_crc_ctx *const *ctxs, int nctx, const 
 int priskv_crc32_ranges_host_multi(priskv_crc_ctx *const *ctxs, int nctx, const void *h_base, uint64_t region_bytes,
                                    const uint64_t *h_offsets, const uint32_t *h_lengths, uint64_t n, uint32_t *h_out)
 {
+    if (!valid_ctxs(ctxs, nctx))
+        return -EINVAL;
     if (n == 0)
-        return (ctxs && nctx >= 1) ? 0 : -EINVAL;
+        return 0;
     if (!h_base || !h_offsets || !h_lengths || !h_out || !region_bytes)
         return -EINVAL;
+    for (uint64_t i = 0; i < n; i++)
+        if (h_offsets[i] > region_bytes || h_lengths[i] > region_bytes - h_offsets[i])
+            return -EINVAL;
+    DevGuard dg(ctxs[0]->device);
+    if (!dg.ok)
+        return -ENODEV;
     MultiJob p{};
     p.base = h_base;
     p.region_bytes = region_bytes;
