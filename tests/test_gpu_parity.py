@@ -324,6 +324,38 @@ def test_bad_args_on_gpu(torch_cuda, ctx):
 
 
 @pytest.mark.slow
+def test_full_size_properties(torch_cuda, ctx):
+    """Size-independent properties at the BASELINE sizes, no CPU oracle:
+    linearity (init 0 / xorout 0: crc(a ^ b) == crc(a) ^ crc(b)) over 1 Mi x
+    4 KiB blocks, and combine consistency: the CRC of each 8 KiB block equals
+    combine(crc(first 4 KiB), crc(second 4 KiB), 4096) from the 4 KiB batch of
+    the same bytes (different kernel plans on each side)."""
+    from priskv_amd import crc32_shift
+    torch = torch_cuda
+    bs, nb = 4096, 1 << 20
+    a = torch.empty(bs * nb, dtype=torch.uint8, device="cuda")
+    b = torch.empty_like(a)
+    ctx.fill_splitmix(a, SEED, 0)
+    ctx.fill_splitmix(b, SEED + 1, 0)
+    ca, cb = ctx.blocks_dev(a, bs), ctx.blocks_dev(b, bs)
+    torch.bitwise_xor(a, b, out=b)
+    cx = ctx.blocks_dev(b, bs)
+    torch.cuda.synchronize()
+    assert np.array_equal(_u32(cx), _u32(ca) ^ _u32(cb))
+    # combine: Z_4096 applied to the first half's CRC as a GF(2) matrix on the host
+    c4 = _u32(ca)
+    c8 = _u32(ctx.blocks_dev(a, 2 * bs))
+    torch.cuda.synchronize()
+    cols = np.array([crc32_shift(1 << i, bs) for i in range(32)], dtype=np.uint32)
+    first = c4[0::2]
+    shifted = np.zeros_like(first)
+    for i in range(32):
+        shifted ^= np.where((first >> np.uint32(i)) & np.uint32(1), cols[i], np.uint32(0)).astype(np.uint32)
+    assert np.array_equal(c8, shifted ^ c4[1::2])
+    del a, b
+
+
+@pytest.mark.slow
 def test_full_config_1M_x_4K(torch_cuda, ctx):
     """BASELINE config 2: 1 Mi x 4 KiB = 4 GiB device-resident, every block
     checked against the oracle run on a D2H copy."""
