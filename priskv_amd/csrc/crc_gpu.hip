@@ -645,6 +645,57 @@ int priskv_crc32_ranges_host_multi(priskv_crc_ctx *const *ctxs, int nctx, const 
 }
 
 // ---- host-streamed path ---------------------------------------------------
+// Pageable input is bounced through pinned staging; one core's memcpy caps
+// that at ~10-15 GB/s, so the copy is split over PRISKV_CRC_COPY_THREADS
+// (default 8) threads.
+struct CopyJob {
+    void *dst;
+    const void *src;
+    size_t n;
+};
+
+static void *copy_worker(void *arg)
+{
+    CopyJob *j = (CopyJob *)arg;
+    memcpy(j->dst, j->src, j->n);
+    return nullptr;
+}
+
+static int copy_threads()
+{
+    static int n = -1;
+    if (n < 0) {
+        const char *e = getenv("PRISKV_CRC_COPY_THREADS");
+        int v = e ? atoi(e) : 8;
+        n = v < 1 ? 1 : (v > 32 ? 32 : v);
+    }
+    return n;
+}
+
+static void par_memcpy(void *dst, const void *src, size_t n)
+{
+    const int T = n >= ((size_t)4 << 20) ? copy_threads() : 1;
+    CopyJob jobs[32];
+    pthread_t th[32];
+    const size_t per = (n / T + 4095) & ~(size_t)4095;
+    int started = 0;
+    for (int t = 0; t < T; t++) {
+        const size_t a = (size_t)t * per;
+        jobs[t].dst = (uint8_t *)dst + (a < n ? a : n);
+        jobs[t].src = (const uint8_t *)src + (a < n ? a : n);
+        jobs[t].n = a < n ? (n - a < per ? n - a : per) : 0;
+    }
+    for (int t = 1; t < T; t++) {
+        if (pthread_create(&th[t], nullptr, copy_worker, &jobs[t]))
+            break;
+        started = t;
+    }
+    copy_worker(&jobs[0]);
+    for (int t = 1; t <= started; t++)
+        pthread_join(th[t], nullptr);
+    for (int t = started + 1; t < T; t++)
+        copy_worker(&jobs[t]);
+}
 static int stream_setup(priskv_crc_ctx *c, uint32_t block_size)
 {
     size_t want = (size_t)64 << 20; // 64 MiB chunks
@@ -729,7 +780,7 @@ int priskv_crc32_blocks_host(priskv_crc_ctx *ctx, const void *h_base, uint64_t n
         const uint8_t *src = (const uint8_t *)h_base + first * block_size;
         const size_t bytes = (size_t)(nb * block_size);
         if (!pinned) {
-            memcpy(ctx->h_bounce[sl], src, bytes);
+            par_memcpy(ctx->h_bounce[sl], src, bytes);
             src = (const uint8_t *)ctx->h_bounce[sl];
         }
         if ((rc = herr(hipMemcpyAsync(ctx->d_stage[sl], src, bytes, hipMemcpyHostToDevice, s))))
