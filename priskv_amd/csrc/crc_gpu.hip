@@ -260,22 +260,29 @@ int launch_blocks(const priskv_crc_ctx *ctx, const uint8_t *base, uint64_t nbloc
     if (path == PATH_ROWS)
         return launch_rows(ctx, base, nblocks, bs, out, s);
     if (path == PATH_SMALL) {
-        const int g = log2u(bs / 16); // G = 1 << g
-        const uint64_t rows = (nblocks * bs + PRV_ROW_BYTES - 1) / PRV_ROW_BYTES;
-        uint64_t want = (rows + 4 * kWaves - 1) / (4 * kWaves);
-        uint32_t grid = (uint32_t)(want < (uint64_t)ctx->max_wgs ? want : (uint64_t)ctx->max_wgs);
-        if (grid == 0)
-            grid = 1;
-        const uint32_t *fold = ctx->d_fold + g * 2048;
-        switch (g) {
-        case 0: hipLaunchKernelGGL(crc_small_kernel<1>, dim3(grid), dim3(kThreads), 0, s, base, nblocks, ctx->d_lds_image[0], fold, out); break;
-        case 1: hipLaunchKernelGGL(crc_small_kernel<2>, dim3(grid), dim3(kThreads), 0, s, base, nblocks, ctx->d_lds_image[0], fold, out); break;
-        case 2: hipLaunchKernelGGL(crc_small_kernel<4>, dim3(grid), dim3(kThreads), 0, s, base, nblocks, ctx->d_lds_image[0], fold, out); break;
-        case 3: hipLaunchKernelGGL(crc_small_kernel<8>, dim3(grid), dim3(kThreads), 0, s, base, nblocks, ctx->d_lds_image[0], fold, out); break;
-        case 4: hipLaunchKernelGGL(crc_small_kernel<16>, dim3(grid), dim3(kThreads), 0, s, base, nblocks, ctx->d_lds_image[0], fold, out); break;
-        default: hipLaunchKernelGGL(crc_small_kernel<32>, dim3(grid), dim3(kThreads), 0, s, base, nblocks, ctx->d_lds_image[0], fold, out); break;
+        const int gl = log2u(bs / 16); // G = 1 << gl
+        const uint64_t per = 1024 / bs; // blocks per row
+        const uint64_t nrows = nblocks / per;
+        if (nrows) {
+            uint64_t want = (nrows + 4 * kWaves - 1) / (4 * kWaves);
+            uint32_t grid = (uint32_t)(want < (uint64_t)ctx->max_wgs ? want : (uint64_t)ctx->max_wgs);
+            const uint32_t *fold = ctx->d_fold + gl * 2048;
+            const uint32_t *img = ctx->d_lds_image[0];
+            switch (gl) {
+            case 0: hipLaunchKernelGGL(crc_small_kernel<1>, dim3(grid), dim3(kThreads), 0, s, base, nrows, img, fold, out); break;
+            case 1: hipLaunchKernelGGL(crc_small_kernel<2>, dim3(grid), dim3(kThreads), 0, s, base, nrows, img, fold, out); break;
+            case 2: hipLaunchKernelGGL(crc_small_kernel<4>, dim3(grid), dim3(kThreads), 0, s, base, nrows, img, fold, out); break;
+            case 3: hipLaunchKernelGGL(crc_small_kernel<8>, dim3(grid), dim3(kThreads), 0, s, base, nrows, img, fold, out); break;
+            case 4: hipLaunchKernelGGL(crc_small_kernel<16>, dim3(grid), dim3(kThreads), 0, s, base, nrows, img, fold, out); break;
+            default: hipLaunchKernelGGL(crc_small_kernel<32>, dim3(grid), dim3(kThreads), 0, s, base, nrows, img, fold, out); break;
+            }
+            if (int rc = herr(hipGetLastError()))
+                return rc;
         }
-        return herr(hipGetLastError());
+        const uint64_t head = nrows * per;
+        if (head == nblocks)
+            return 0;
+        return launch_generic(ctx, base + head * bs, nblocks - head, bs, bs, nullptr, nullptr, out + head, s);
     }
     if (bs >= PRV_ROW_BYTES)
         return launch_extents(ctx, base, nblocks, nullptr, nullptr, bs, bs, out, s);
