@@ -177,16 +177,20 @@ int main(int argc, char **argv)
 
     std::vector<Variant> all;
     // first entry = product reference for the bit-exact cross-check and the sustained run
-    all.push_back(CRC_VARIANT(32, 8, 2, 2, 1, 0));
     all.push_back(CRC_VARIANT(32, 8, 2, 2, 1, 2));
+    all.push_back(CRC_VARIANT(32, 8, 2, 2, 1, 0));
     all.push_back(CRC_VARIANT(32, 8, 2, 2, 1, 3));
-    all.push_back(CRC_VARIANT(16, 16, 2, 2, 1, 0));
-    all.push_back(CRC_VARIANT(16, 16, 2, 2, 1, 2));
-    all.push_back(CRC_VARIANT(16, 16, 2, 2, 1, 3));
     all.push_back(CRC_VARIANT(32, 8, 2, 2, 2, 2));
+    all.push_back(CRC_VARIANT(16, 16, 2, 2, 1, 2));
     all.push_back(CRC_VARIANT(64, 4, 2, 2, 1, 0));
-    all.push_back(CRC_VARIANT(64, 4, 2, 2, 2, 2));
-    all.push_back(CRC_VARIANT(64, 4, 2, 2, 1, 2));
+    all.push_back(CRC_VARIANT(64, 4, 2, 2, 2, 0));
+    all.push_back(CRC2_VARIANT(32, 4, 2, 2, 1));
+    all.push_back(CRC2_VARIANT(64, 2, 2, 2, 1));
+    // compute ceilings (no memory traffic after the prologue; CRCs meaningless)
+    all.push_back(CRC_VARIANT(32, 8, 2, 2, 1, 6));
+    all.push_back(CRC_VARIANT(32, 8, 2, 2, 2, 6));
+    all.push_back(CRC_VARIANT(64, 4, 2, 2, 1, 4));
+    all.push_back(CRC_VARIANT(64, 4, 2, 2, 2, 4));
     all.push_back(ROOF_VARIANT(64, 4, 2, 2, 2));
     all.push_back(ROOF_VARIANT(64, 4, 2, 2, 1));
     all.push_back(ROOF_VARIANT(32, 8, 2, 2, 1));
@@ -216,7 +220,8 @@ int main(int argc, char **argv)
     std::vector<Variant> V;
     for (auto &v : all)
         if (keep(v.name) && bs % (uint32_t)(v.CH * 16 * v.G) == 0 && nb % (2 * 64 / v.G) == 0 &&
-            (!strstr(v.name, "opt2") && !strstr(v.name, "opt3") || bs == (uint32_t)(v.CH * 16 * v.G)))
+            (!strstr(v.name, "opt2") && !strstr(v.name, "opt3") && !strstr(v.name, "opt6") ||
+             bs == (uint32_t)(v.CH * 16 * v.G)))
             V.push_back(v);
     Variant gs{"roof gridstride nt", false, 64, 1, 8, nullptr, {}};
 
@@ -246,7 +251,7 @@ int main(int argc, char **argv)
             CK(hipEventElapsedTime(&ms, e0, e1));
             if (r > 0)
                 v.ms.push_back(ms / iters);
-            if (vi < V.size() && v.is_crc && r == 0) {
+            if (vi < V.size() && v.is_crc && r == 0 && !strstr(v.name, "opt4") && !strstr(v.name, "opt6")) {
                 if (vi == 0)
                     CK(hipMemcpy(d_ref, d_out, nb * 4, hipMemcpyDeviceToDevice));
                 else {
