@@ -59,6 +59,7 @@ struct priskv_crc_ctx {
     uint32_t *d_lds_image[3];  // 64 KiB each: set B gap for G = 64, 32, 16
     uint32_t *d_fold;          // kFoldSets x 2048 words, set j for G = 1 << j
     uint32_t *d_sarwate;       // 256 words
+    uint32_t *d_unshift;       // 16 x 32 words: columns of Z_-p, p = 0..15
     // host-streamed path (guarded by lock)
     pthread_mutex_t lock;
     int stream_ready;
@@ -140,6 +141,10 @@ int launch_generic(const priskv_crc_ctx *ctx, const uint8_t *base, uint64_t n, u
     return herr(hipGetLastError());
 }
 
+constexpr int kNbuf = 2;  // register pipeline depth (chunks)
+constexpr int kAux = 2;   // cache policy of the streaming loads: nt
+constexpr int kExtRows = 4; // rows per chunk of the extents kernel
+
 // extents through the row machinery (any base alignment, any lengths)
 int launch_extents(const priskv_crc_ctx *ctx, const uint8_t *base, uint64_t n, const uint64_t *offs,
                    const uint32_t *lens, uint64_t stride, uint32_t len_const, uint32_t *out, hipStream_t s)
@@ -149,8 +154,9 @@ int launch_extents(const priskv_crc_ctx *ctx, const uint8_t *base, uint64_t n, c
     const uint64_t want = (n + kWaves - 1) / kWaves;
     const uint64_t cap = (uint64_t)ctx->num_cus * 2;
     const uint32_t grid = (uint32_t)(want < cap ? want : cap);
-    hipLaunchKernelGGL(crc_ranges_kernel, dim3(grid), dim3(kThreads), 0, s, abase, n, offs, lens, shift, stride,
-                       len_const, ctx->d_lds_image[0], ctx->d_fold + 6 * 2048, ctx->d_sarwate, out);
+    hipLaunchKernelGGL((crc_ranges_kernel<kExtRows, kNbuf, kAux>), dim3(grid), dim3(kThreads), 0, s, abase, n, offs,
+                       lens, shift, stride, len_const, ctx->d_lds_image[0], ctx->d_fold + 6 * 2048, ctx->d_unshift,
+                       out);
     return herr(hipGetLastError());
 }
 
@@ -158,8 +164,6 @@ int launch_extents(const priskv_crc_ctx *ctx, const uint8_t *base, uint64_t n, c
 // (G lanes per block, CH rows per chunk, workgroups per CU) by block size,
 // from the tools/crc_explore sweeps recorded in DESIGN.md §5.  Pipeline depth
 // (NBUF = 2) and cache policy (nt) are fixed.
-constexpr int kNbuf = 2;
-constexpr int kAux = 2;
 
 enum PlanId {
     PLAN_G32_CH8_PIPE, // 4 KiB: one chunk == one 2-block group, fold pipelined
@@ -236,8 +240,53 @@ int launch_plan(const priskv_crc_ctx *ctx, int p, const uint8_t *base, uint64_t 
     return 0;
 }
 
+// Few large blocks: the rows kernel splits block GROUPS statically over the
+// resident waves, so 1024 x 1 MiB (1024 groups for 2048 waves) leaves half
+// the chip idle and 3000 groups run at 3000/(2*2048) = 73 %.  Such batches
+// are hashed as S equal segments per block (S a power of two, segments
+// >= 16 KiB and whole 1 KiB rows) until there are >= 8 groups per wave, and
+// the segment CRCs are combined by crc_combine_segments_kernel.
+constexpr uint64_t kGroupsPerWave = 8;
+constexpr uint32_t kMinSegment = 16u << 10;
+
+uint32_t segments_for(const priskv_crc_ctx *ctx, uint64_t nblocks, uint32_t bs)
+{
+    const uint64_t want = (uint64_t)ctx->num_cus * kWaves * kGroupsPerWave;
+    uint32_t S = 1;
+    while (nblocks * S < want && bs / (2 * S) >= kMinSegment && (bs / (2 * S)) % PRV_ROW_BYTES == 0 &&
+           bs % (2 * S) == 0)
+        S *= 2;
+    return S;
+}
+
+int launch_rows_plain(const priskv_crc_ctx *ctx, const uint8_t *base, uint64_t nblocks, uint32_t bs, uint32_t *out,
+                      hipStream_t s);
+
 int launch_rows(const priskv_crc_ctx *ctx, const uint8_t *base, uint64_t nblocks, uint32_t bs, uint32_t *out,
                 hipStream_t s)
+{
+    const uint32_t S = segments_for(ctx, nblocks, bs);
+    if (S == 1)
+        return launch_rows_plain(ctx, base, nblocks, bs, out, s);
+    // stream-ordered scratch: concurrent calls on other streams never share it
+    uint32_t *sub = nullptr;
+    if (int rc = herr(hipMallocAsync((void **)&sub, nblocks * S * sizeof(uint32_t), s)))
+        return rc;
+    int rc = launch_rows_plain(ctx, base, nblocks * S, bs / S, sub, s);
+    if (!rc) {
+        ZCols z;
+        prv_shift_columns(z.c, bs / S);
+        const uint64_t want = (nblocks + 255) / 256;
+        const uint32_t grid = (uint32_t)(want < (uint64_t)ctx->num_cus * 4 ? want : (uint64_t)ctx->num_cus * 4);
+        hipLaunchKernelGGL(crc_combine_segments_kernel, dim3(grid), dim3(256), 0, s, sub, nblocks, S, z, out);
+        rc = herr(hipGetLastError());
+    }
+    const int frc = herr(hipFreeAsync(sub, s));
+    return rc ? rc : frc;
+}
+
+int launch_rows_plain(const priskv_crc_ctx *ctx, const uint8_t *base, uint64_t nblocks, uint32_t bs, uint32_t *out,
+                      hipStream_t s)
 {
     const int p = plan_for(bs);
     const uint64_t per = 64 / kPlans[p].G; // blocks per wave group
@@ -335,6 +384,7 @@ int priskv_crc_ctx_create(int device, priskv_crc_ctx **out)
     uint32_t *h_img = (uint32_t *)malloc(sizeof(uint32_t) * PRV_LDS_WORDS);
     uint32_t *h_fold = (uint32_t *)malloc(sizeof(uint32_t) * 2048 * kFoldSets);
     uint32_t h_sar[256];
+    uint32_t h_unshift[16 * 32];
     if (!h_img || !h_fold) {
         rc = -ENOMEM;
         goto fail;
@@ -345,11 +395,14 @@ int priskv_crc_ctx_create(int device, priskv_crc_ctx **out)
     for (int j = 0; j < kFoldSets; j++)
         prv_fold_columns(h_fold + j * 2048, 1u << j);
     prv_sarwate_table(h_sar);
+    prv_unshift_columns(h_unshift);
     if ((rc = herr(hipMalloc((void **)&c->d_fold, sizeof(uint32_t) * 2048 * kFoldSets))) ||
-        (rc = herr(hipMalloc((void **)&c->d_sarwate, sizeof(h_sar)))))
+        (rc = herr(hipMalloc((void **)&c->d_sarwate, sizeof(h_sar)))) ||
+        (rc = herr(hipMalloc((void **)&c->d_unshift, sizeof(h_unshift)))))
         goto fail;
     if ((rc = herr(hipMemcpy(c->d_fold, h_fold, sizeof(uint32_t) * 2048 * kFoldSets, hipMemcpyHostToDevice))) ||
-        (rc = herr(hipMemcpy(c->d_sarwate, h_sar, sizeof(h_sar), hipMemcpyHostToDevice))))
+        (rc = herr(hipMemcpy(c->d_sarwate, h_sar, sizeof(h_sar), hipMemcpyHostToDevice))) ||
+        (rc = herr(hipMemcpy(c->d_unshift, h_unshift, sizeof(h_unshift), hipMemcpyHostToDevice))))
         goto fail;
     for (int gi = 0; gi < 3; gi++) {
         const uint32_t G = 64u >> gi; // 64, 32, 16
@@ -392,6 +445,7 @@ void priskv_crc_ctx_destroy(priskv_crc_ctx *c)
         (void)hipFree(c->d_lds_image[gi]);
     (void)hipFree(c->d_fold);
     (void)hipFree(c->d_sarwate);
+    (void)hipFree(c->d_unshift);
     (void)hipFree(c->d_scrub);
     if (c->aux)
         (void)hipStreamDestroy(c->aux);

@@ -148,6 +148,30 @@ void prv_fold_columns(uint32_t out[32 * 64], uint32_t group)
     }
 }
 
+/* one zero byte backwards: c' = T[c & 0xff] ^ (c >> 8) has top byte
+ * T[c & 0xff] >> 24, and the top bytes of the 256 table entries are distinct,
+ * so c & 0xff = b with T[b] >> 24 == c' >> 24 and c = ((c' ^ T[b]) << 8) | b */
+static uint32_t unshift_byte(uint32_t c, const uint8_t inv_top[256])
+{
+    const uint32_t b = inv_top[c >> 24];
+    return ((c ^ g_slice[0][b]) << 8) | b;
+}
+
+void prv_unshift_columns(uint32_t out[16 * 32])
+{
+    pthread_once(&g_once, host_init);
+    uint8_t inv_top[256];
+    for (uint32_t b = 0; b < 256; b++)
+        inv_top[g_slice[0][b] >> 24] = (uint8_t)b;
+    for (int i = 0; i < 32; i++) {
+        uint32_t v = 1u << i;
+        for (int p = 0; p < 16; p++) {
+            out[p * 32 + i] = v; /* column i of Z_-p */
+            v = unshift_byte(v, inv_top);
+        }
+    }
+}
+
 void prv_sarwate_table(uint32_t out[256])
 {
     pthread_once(&g_once, host_init);

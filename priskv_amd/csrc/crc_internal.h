@@ -24,6 +24,8 @@ PRV_HIDDEN void prv_lds_image(uint32_t out[PRV_LDS_WORDS], uint32_t gap_bytes);
 PRV_HIDDEN void prv_fold_columns(uint32_t out[32 * 64], uint32_t group);
 PRV_HIDDEN void prv_shift_columns(uint32_t out[32], uint64_t nbytes);
 PRV_HIDDEN void prv_sarwate_table(uint32_t out[256]);
+/* out[p*32 + i] = column i of Z_-p (p = 0..15): undoes p trailing zero bytes */
+PRV_HIDDEN void prv_unshift_columns(uint32_t out[16 * 32]);
 
 #if defined(__cplusplus)
 }

@@ -197,6 +197,42 @@ def test_ranges_edges(torch_cuda, ctx):
     assert np.array_equal(_u32(out2), O.crc32_ranges(view.cpu().numpy(), o2, l2))
 
 
+def test_ranges_chunk_boundaries(torch_cuda, ctx):
+    """Extents whose row count crosses the extents kernel's 4-row chunk edges
+    (lengths m*4 KiB +- 0..17 at every 16-B start phase): leading virtual rows,
+    the trailing pad p = 0..15 undone by Z_-p, and head + tail masks in one row."""
+    torch = torch_cuda
+    n = 1 << 17
+    t = torch.empty(n, dtype=torch.uint8, device="cuda")
+    ctx.fill_splitmix(t, SEED, 21)
+    offs, lens = [], []
+    for phase in range(16):
+        for m in range(4):
+            for d in range(-17, 18):
+                ln = m * 4096 + d
+                if ln >= 0:
+                    offs.append(4096 * (1 + m) + phase)
+                    lens.append(ln)
+    o = np.array(offs, dtype=np.uint64)
+    ln = np.array(lens, dtype=np.uint32)
+    out = ctx.ranges_dev(t, torch.from_numpy(o.astype(np.int64)).cuda(), torch.from_numpy(ln.view(np.int32)).cuda())
+    torch.cuda.synchronize()
+    assert np.array_equal(_u32(out), O.crc32_ranges(t.cpu().numpy(), o, ln))
+
+
+@pytest.mark.parametrize("bs,nb", [(1 << 20, 1), (1 << 20, 3), (1 << 20, 100), (2 << 20, 5), (4 << 20, 2),
+                                   (48 << 10, 7), (3 << 20, 1), (1025 << 10, 3), (96 << 10, 1000)])
+def test_segmented_large_blocks(torch_cuda, ctx, bs, nb):
+    """Batches of few large blocks are hashed as equal segments and combined
+    with Z_seg (crc_combine_segments_kernel); results must not change."""
+    torch = torch_cuda
+    t = _region(torch, ctx, bs * nb, SEED ^ 0x51, nb)
+    out = ctx.blocks_dev(t, bs, nblocks=nb)
+    torch.cuda.synchronize()
+    want = O.crc32_blocks(t[: bs * nb].cpu().numpy(), bs, nthreads=8)
+    assert np.array_equal(_u32(out), want), (bs, nb)
+
+
 def test_ranges_beyond_2GiB_and_many_per_wave(torch_cuda, ctx):
     """Extents at offsets with bit 31 (and bit 32) set, and far more extents
     than waves so each wave loops over many of them (a sign-extension of the
