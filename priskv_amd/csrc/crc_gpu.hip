@@ -143,7 +143,7 @@ int launch_generic(const priskv_crc_ctx *ctx, const uint8_t *base, uint64_t n, u
 
 constexpr int kNbuf = 2;  // register pipeline depth (chunks)
 constexpr int kAux = 2;   // cache policy of the streaming loads: nt
-constexpr int kExtRows = 4; // rows per chunk of the extents kernel
+constexpr int kExtRows = 2; // rows per chunk of the extents kernel (tools/ranges_explore)
 
 // extents through the row machinery (any base alignment, any lengths)
 int launch_extents(const priskv_crc_ctx *ctx, const uint8_t *base, uint64_t n, const uint64_t *offs,
