@@ -120,9 +120,10 @@ int priskv_crc_fill_splitmix_dev(const priskv_crc_ctx *ctx, void *d_dst, uint64_
                                  uint64_t seed, uint64_t word_offset, void *stream);
 
 /* Which kernel a (d_base, block_size) batch dispatches to: 1 = rows (block
- * a multiple of 1 KiB, 16-byte aligned base: G = 16/32/64 lanes per block),
+ * a multiple of 1 KiB, 16-byte aligned base: G = 16/32/64 lanes per block;
+ * batches of few large blocks are hashed as segments and combined),
  * 2 = extents (any other block >= 1 KiB or any base alignment: one wave per
- * block, masked rows + byte-serial tail), 3 = sub-KiB power-of-two blocks,
+ * block, masked right-aligned rows + Z_-p tail), 3 = sub-KiB power-of-two blocks,
  * 4 = generic (smaller odd sizes: one thread per block).  For tests and
  * benchmarks; -EINVAL for invalid arguments. */
 int priskv_crc32_blocks_path(const void *d_base, uint64_t nblocks, uint32_t block_size);
