@@ -22,10 +22,11 @@
 
 namespace {
 #include "../priskv_amd/csrc/crc_device.inc"
+#include "crc_dyn_explore.inc"
 
 // read-only roof with the rows kernel's loop and addressing (same loads, no hashing)
 template <int G, int CH, int NBUF, int AUX>
-__global__ __launch_bounds__(kThreads, 2) void roof_rows(const uint8_t *__restrict__ base, uint64_t ngroups,
+__global__ __launch_bounds__(kThreads, rows_min_wg(CH, NBUF)) void roof_rows(const uint8_t *__restrict__ base, uint64_t ngroups,
                                                          uint32_t block_size, const uint32_t *, const uint32_t *,
                                                          uint32_t *__restrict__ out)
 {
@@ -118,27 +119,40 @@ struct Variant {
     const char *name;
     bool is_crc;
     int G, CH, wg_per_cu;
+    int opt; // crc_rows_kernel OPT bits (-1: not a rows-kernel CRC variant)
     void (*launch)(dim3, hipStream_t, const uint8_t *, uint64_t, uint32_t, const uint32_t *, const uint32_t *,
                    uint32_t *);
     std::vector<float> ms;
 };
 
 #define CRC_VARIANT(G, CH, NB, AUX, WGPC, OPT)                                                                 \
-    Variant{"crc G" #G " CH" #CH " NBUF" #NB " AUX" #AUX " wg/cu" #WGPC " opt" #OPT, true, G, CH, WGPC,       \
+    Variant{"crc G" #G " CH" #CH " NBUF" #NB " AUX" #AUX " wg/cu" #WGPC " opt" #OPT, true, G, CH, WGPC, OPT,  \
             [](dim3 g, hipStream_t s, const uint8_t *b, uint64_t n, uint32_t bs, const uint32_t *img,           \
                const uint32_t *fold, uint32_t *o) {                                                            \
                 hipLaunchKernelGGL((crc_rows_kernel<G, CH, NB, AUX, OPT>), g, dim3(kThreads), 0, s, b, n, bs, img, \
                                    fold, o);                                                                   \
             }, {}}
 #define CRC2_VARIANT(G, CH, NB, AUX, WGPC)                                                                     \
-    Variant{"crc2 G" #G " CH" #CH " NBUF" #NB " AUX" #AUX " wg/cu" #WGPC, true, G, CH, WGPC,                \
+    Variant{"crc2 G" #G " CH" #CH " NBUF" #NB " AUX" #AUX " wg/cu" #WGPC, true, G, CH, WGPC, -1,            \
             [](dim3 g, hipStream_t s, const uint8_t *b, uint64_t n, uint32_t bs, const uint32_t *img,           \
                const uint32_t *fold, uint32_t *o) {                                                            \
                 hipLaunchKernelGGL((crc_rows2_kernel<G, CH, NB, AUX>), g, dim3(kThreads), 0, s, b, n / 2, bs, img, \
                                    fold, o);                                                                   \
             }, {}}
+// dynamically balanced variants: tile size and ticket counter via globals
+static uint32_t *g_ctr = nullptr;
+#define DYN_VARIANT(G, CH, NB, AUX, WGPC, OPT)                                                                 \
+    Variant{((OPT) & 16 ? "roof dyn G" #G " CH" #CH " NBUF" #NB " wg/cu" #WGPC                                 \
+                        : "crc dyn G" #G " CH" #CH " NBUF" #NB " wg/cu" #WGPC " opt" #OPT),                     \
+            !((OPT) & 16), G, CH, WGPC, -1,                                                                    \
+            [](dim3 g, hipStream_t s, const uint8_t *b, uint64_t n, uint32_t bs, const uint32_t *img,           \
+               const uint32_t *fold, uint32_t *o) {                                                            \
+                (void)hipMemsetAsync(g_ctr, 0, 4, s);                                                          \
+                hipLaunchKernelGGL((crc_rows_dyn_kernel<G, CH, NB, AUX, OPT>), g, dim3(kThreads), 0, s, b, n, bs, \
+                                   img, fold, o, g_ctr);                                                       \
+            }, {}}
 #define ROOF_VARIANT(G, CH, NB, AUX, WGPC)                                                                 \
-    Variant{"roof G" #G " CH" #CH " NBUF" #NB " AUX" #AUX " wg/cu" #WGPC, false, G, CH, WGPC,             \
+    Variant{"roof G" #G " CH" #CH " NBUF" #NB " AUX" #AUX " wg/cu" #WGPC, false, G, CH, WGPC, -1,         \
             [](dim3 g, hipStream_t s, const uint8_t *b, uint64_t n, uint32_t bs, const uint32_t *img,       \
                const uint32_t *fold, uint32_t *o) {                                                        \
                 hipLaunchKernelGGL((roof_rows<G, CH, NB, AUX>), g, dim3(kThreads), 0, s, b, n, bs, img, fold, o); \
@@ -168,33 +182,29 @@ int main(int argc, char **argv)
         CK(hipMemcpy(d_fold[G], fold.data(), fold.size() * 4, hipMemcpyHostToDevice));
     }
     CK(hipMalloc(&d, (size_t)bs * nb));
-    CK(hipMalloc(&d_out, nb * 4));
+    CK(hipMalloc(&d_out, nb * 4 + (size_t)ncu * 4 * kWaves * 8)); // + per-wave timestamps
     CK(hipMalloc(&d_ref, nb * 4));
     CK(hipMalloc(&d_sink, (size_t)ncu * 16 * 1024 * 4));
     hipLaunchKernelGGL(fill_splitmix_kernel, dim3(ncu * 16), dim3(256), 0, 0, d, (uint64_t)bs * nb, 0x5EED5EEDull,
                        0ull);
     CK(hipDeviceSynchronize());
 
+    CK(hipMalloc(&g_ctr, 64));
     std::vector<Variant> all;
     // first entry = product reference for the bit-exact cross-check and the sustained run
     all.push_back(CRC_VARIANT(32, 8, 2, 2, 1, 2));
-    all.push_back(CRC_VARIANT(32, 8, 2, 2, 1, 0));
-    all.push_back(CRC_VARIANT(32, 8, 2, 2, 1, 3));
-    all.push_back(CRC_VARIANT(32, 8, 2, 2, 2, 2));
-    all.push_back(CRC_VARIANT(16, 16, 2, 2, 1, 2));
+    all.push_back(CRC_VARIANT(32, 8, 2, 2, 1, 34));
+    all.push_back(CRC_VARIANT(32, 8, 2, 2, 1, 66));
+    all.push_back(CRC_VARIANT(32, 8, 3, 2, 1, 2));
+    all.push_back(CRC_VARIANT(32, 8, 3, 2, 1, 34));
+    all.push_back(CRC_VARIANT(32, 8, 2, 2, 1, 10));
+    all.push_back(CRC_VARIANT(32, 8, 2, 2, 1, 42));
     all.push_back(CRC_VARIANT(64, 4, 2, 2, 1, 0));
-    all.push_back(CRC_VARIANT(64, 4, 2, 2, 2, 0));
-    all.push_back(CRC2_VARIANT(32, 4, 2, 2, 1));
-    all.push_back(CRC2_VARIANT(64, 2, 2, 2, 1));
-    // compute ceilings (no memory traffic after the prologue; CRCs meaningless)
-    all.push_back(CRC_VARIANT(32, 8, 2, 2, 1, 6));
-    all.push_back(CRC_VARIANT(32, 8, 2, 2, 2, 6));
-    all.push_back(CRC_VARIANT(64, 4, 2, 2, 1, 4));
-    all.push_back(CRC_VARIANT(64, 4, 2, 2, 2, 4));
-    all.push_back(ROOF_VARIANT(64, 4, 2, 2, 2));
-    all.push_back(ROOF_VARIANT(64, 4, 2, 2, 1));
+    all.push_back(CRC_VARIANT(64, 4, 2, 2, 1, 32));
+    all.push_back(CRC_VARIANT(64, 4, 2, 2, 1, 8));
+    all.push_back(CRC_VARIANT(64, 4, 2, 2, 1, 40));
     all.push_back(ROOF_VARIANT(32, 8, 2, 2, 1));
-    all.push_back(ROOF_VARIANT(16, 8, 2, 2, 2));
+    all.push_back(ROOF_VARIANT(64, 4, 2, 2, 2));
     // EXPLORE_FILTER="a,b,c": keep only variants whose name contains one of the substrings
     std::vector<std::string> filt;
     if (const char *f = getenv("EXPLORE_FILTER")) {
@@ -220,10 +230,9 @@ int main(int argc, char **argv)
     std::vector<Variant> V;
     for (auto &v : all)
         if (keep(v.name) && bs % (uint32_t)(v.CH * 16 * v.G) == 0 && nb % (2 * 64 / v.G) == 0 &&
-            (!strstr(v.name, "opt2") && !strstr(v.name, "opt3") && !strstr(v.name, "opt6") ||
-             bs == (uint32_t)(v.CH * 16 * v.G)))
+            (v.opt < 0 || !(v.opt & 2) || bs == (uint32_t)(v.CH * 16 * v.G)))
             V.push_back(v);
-    Variant gs{"roof gridstride nt", false, 64, 1, 8, nullptr, {}};
+    Variant gs{"roof gridstride nt", false, 64, 1, 8, -1, nullptr, {}};
 
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
@@ -251,7 +260,7 @@ int main(int argc, char **argv)
             CK(hipEventElapsedTime(&ms, e0, e1));
             if (r > 0)
                 v.ms.push_back(ms / iters);
-            if (vi < V.size() && v.is_crc && r == 0 && !strstr(v.name, "opt4") && !strstr(v.name, "opt6")) {
+            if (vi < V.size() && v.is_crc && r == 0 && !(v.opt > 0 && (v.opt & 4))) { // bit 2: no-load ceiling
                 if (vi == 0)
                     CK(hipMemcpy(d_ref, d_out, nb * 4, hipMemcpyDeviceToDevice));
                 else {
@@ -302,6 +311,43 @@ int main(int argc, char **argv)
         }
         std::sort(t.begin(), t.end());
         printf("\n  min %.4f  median %.4f  max %.4f ms\n", t[0], t[n / 2], t[n - 1]);
+    }
+    // per-wave start / end spread of the timing variants (OPT bit 3)
+    for (auto &v : V) {
+        if (v.opt < 0 || !(v.opt & 8))
+            continue;
+        const uint64_t ng = nb / (64 / v.G);
+        const uint64_t want = (ng + kWaves - 1) / kWaves;
+        const uint32_t grid = (uint32_t)std::min<uint64_t>(want, (uint64_t)ncu * v.wg_per_cu);
+        const uint32_t W = grid * kWaves;
+        for (int rep = 0; rep < 3; rep++) {
+            v.launch(dim3(grid), 0, d, ng, bs, d_img[v.G], d_fold[v.G], d_out);
+            CK(hipDeviceSynchronize());
+            std::vector<uint32_t> ts(2 * W);
+            CK(hipMemcpy(ts.data(), d_out + nb, ts.size() * 4, hipMemcpyDeviceToHost));
+            uint32_t t0 = ts[0];
+            for (uint32_t w = 0; w < W; w++)
+                t0 = std::min(t0, ts[2 * w]);
+            std::vector<double> st(W), en(W), xe(8, 0.0);
+            std::vector<int> xn(8, 0);
+            for (uint32_t w = 0; w < W; w++) {
+                st[w] = (ts[2 * w] - t0) * 0.01;     // us (100 MHz)
+                en[w] = (ts[2 * w + 1] - t0) * 0.01;
+                xe[(w / kWaves) % 8] += en[w];
+                xn[(w / kWaves) % 8]++;
+            }
+            std::vector<double> s2 = st, e2 = en;
+            std::sort(s2.begin(), s2.end());
+            std::sort(e2.begin(), e2.end());
+            auto pc = [&](std::vector<double> &a, double q) { return a[(size_t)(q * (a.size() - 1))]; };
+            printf("timing %s rep %d: start p50 %.1f p100 %.1f us | end p0 %.1f p10 %.1f p50 %.1f p90 %.1f "
+                   "p99 %.1f p100 %.1f us | mean end by XCD:",
+                   v.name, rep, pc(s2, 0.5), pc(s2, 1.0), pc(e2, 0.0), pc(e2, 0.1), pc(e2, 0.5), pc(e2, 0.9),
+                   pc(e2, 0.99), pc(e2, 1.0));
+            for (int x = 0; x < 8; x++)
+                printf(" %.1f", xn[x] ? xe[x] / xn[x] : 0.0);
+            printf("\n");
+        }
     }
     return ok_all ? 0 : 1;
 }
