@@ -56,6 +56,7 @@ struct priskv_crc_ctx {
     int num_cus;
     int max_wgs;               // resident workgroups of the sub-KiB kernel (2 per CU)
     int plan_wgs_per_cu[8];    // resident workgroups per CU of each rows-kernel plan
+    uint32_t xcd_weights;      // rows-kernel split: (even << 16) | odd XCD weight, 0 = equal
     uint32_t *d_lds_image[3];  // 64 KiB each: set B gap for G = 64, 32, 16
     uint32_t *d_fold;          // kFoldSets x 2048 words, set j for G = 1 << j
     uint32_t *d_sarwate;       // 256 words
@@ -232,7 +233,9 @@ int launch_plan(const priskv_crc_ctx *ctx, int p, const uint8_t *base, uint64_t 
         uint32_t *o = out + done * nb_per_group;
         const uint32_t *img = ctx->d_lds_image[gi];
         const uint32_t *fold = ctx->d_fold + log2u(P.G) * 2048;
-        void *args[] = {(void *)&b, (void *)&n, (void *)&bs, (void *)&img, (void *)&fold, (void *)&o};
+        // weights move whole groups: only worth it with many groups per wave
+        uint32_t xw = n >= 32ull * grid * kWaves ? ctx->xcd_weights : 0u;
+        void *args[] = {(void *)&b, (void *)&n, (void *)&bs, (void *)&img, (void *)&fold, (void *)&o, (void *)&xw};
         if (int rc = herr(hipLaunchKernel(plan_fn(p), dim3(grid), dim3(kThreads), args, 0, s)))
             return rc;
         done += n;
@@ -242,18 +245,24 @@ int launch_plan(const priskv_crc_ctx *ctx, int p, const uint8_t *base, uint64_t 
 
 // Few large blocks: the rows kernel splits block GROUPS statically over the
 // resident waves, so 1024 x 1 MiB (1024 groups for 2048 waves) leaves half
-// the chip idle and 3000 groups run at 3000/(2*2048) = 73 %.  Such batches
-// are hashed as S equal segments per block (S a power of two, segments
-// >= 16 KiB and whole 1 KiB rows) until there are >= 8 groups per wave, and
-// the segment CRCs are combined by crc_combine_segments_kernel.
-constexpr uint64_t kGroupsPerWave = 8;
+// the chip idle and 3000 groups run at 3000 / (2 * 2048) = 73 % balance.
+// When that balance r / ceil(r) (r = groups per resident wave) is below
+// 0.9, each block is hashed as S equal segments (S a power of two, segments
+// >= 16 KiB and whole 1 KiB rows), doubling S until the balance is reached,
+// and the segment CRCs are combined by crc_combine_segments_kernel.
 constexpr uint32_t kMinSegment = 16u << 10;
+
+bool balanced(uint64_t units, uint64_t waves)
+{
+    const uint64_t c = (units + waves - 1) / waves; // units of the busiest wave
+    return units * 10 >= c * waves * 9;
+}
 
 uint32_t segments_for(const priskv_crc_ctx *ctx, uint64_t nblocks, uint32_t bs)
 {
-    const uint64_t want = (uint64_t)ctx->num_cus * kWaves * kGroupsPerWave;
+    const uint64_t waves = (uint64_t)ctx->num_cus * kWaves; // 1 WG/CU: the plans for blocks > 16 KiB
     uint32_t S = 1;
-    while (nblocks * S < want && bs / (2 * S) >= kMinSegment && (bs / (2 * S)) % PRV_ROW_BYTES == 0 &&
+    while (!balanced(nblocks * S, waves) && bs / (2 * S) >= kMinSegment && (bs / (2 * S)) % PRV_ROW_BYTES == 0 &&
            bs % (2 * S) == 0)
         S *= 2;
     return S;
@@ -338,6 +347,26 @@ int launch_blocks(const priskv_crc_ctx *ctx, const uint8_t *base, uint64_t nbloc
     return launch_generic(ctx, base, nblocks, bs, bs, nullptr, nullptr, out, s);
 }
 
+// XCD weights of the rows-kernel split: on a multi-XCD device
+// (workgroups dispatched round-robin over 8 XCDs) waves on odd XCDs finish
+// ~10 % later under an equal split on every MI355X measured, so even-XCD
+// waves take 31 parts to odd 29.  PRISKV_CRC_XCD_WEIGHTS="we:wo" overrides
+// ("1:1" = equal split).
+uint32_t xcd_weights(int num_cus)
+{
+    uint32_t we = 31, wo = 29;
+    if (num_cus < 64 || num_cus % 8) // one XCD (or a partition mode): nothing to balance
+        we = wo = 1;
+    if (const char *e = getenv("PRISKV_CRC_XCD_WEIGHTS")) {
+        unsigned a = 0, b = 0;
+        if (sscanf(e, "%u:%u", &a, &b) == 2 && a && b && a < 65536 && b < 65536) {
+            we = a;
+            wo = b;
+        }
+    }
+    return we == wo ? 0u : ((we << 16) | wo);
+}
+
 // resident workgroups per CU of every plan: the plan's choice, capped by
 // what the runtime can actually co-schedule (VGPR / LDS limits)
 int rows_occupancy(priskv_crc_ctx *c)
@@ -392,6 +421,7 @@ int priskv_crc_ctx_create(int device, priskv_crc_ctx **out)
     if ((rc = herr(hipDeviceGetAttribute(&c->num_cus, hipDeviceAttributeMultiprocessorCount, device))))
         goto fail;
     c->max_wgs = 2 * c->num_cus;
+    c->xcd_weights = xcd_weights(c->num_cus);
     for (int j = 0; j < kFoldSets; j++)
         prv_fold_columns(h_fold + j * 2048, 1u << j);
     prv_sarwate_table(h_sar);

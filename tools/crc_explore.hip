@@ -28,15 +28,15 @@ namespace {
 template <int G, int CH, int NBUF, int AUX>
 __global__ __launch_bounds__(kThreads, rows_min_wg(CH, NBUF)) void roof_rows(const uint8_t *__restrict__ base, uint64_t ngroups,
                                                          uint32_t block_size, const uint32_t *, const uint32_t *,
-                                                         uint32_t *__restrict__ out)
+                                                         uint32_t *__restrict__ out, uint32_t xw)
 {
     constexpr int NB = 64 / G, RB = 16 * G;
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint64_t W = (uint64_t)gridDim.x * kWaves;
     const uint64_t wid = (uint64_t)blockIdx.x * kWaves + wave;
-    const uint64_t g0 = uniform64(ngroups * wid / W);
-    const uint64_t ng = ngroups * (wid + 1) / W - g0;
+    uint64_t g0, ng;
+    wave_range(ngroups, W, wid, xw, g0, ng);
     if (ng == 0)
         return;
     const uint32_t cps = block_size / (CH * RB);
@@ -125,13 +125,15 @@ struct Variant {
     std::vector<float> ms;
 };
 
-#define CRC_VARIANT(G, CH, NB, AUX, WGPC, OPT)                                                                 \
-    Variant{"crc G" #G " CH" #CH " NBUF" #NB " AUX" #AUX " wg/cu" #WGPC " opt" #OPT, true, G, CH, WGPC, OPT,  \
+#define CRC_VARIANT_W(G, CH, NB, AUX, WGPC, OPT, WE, WO)                                                      \
+    Variant{"crc G" #G " CH" #CH " NBUF" #NB " AUX" #AUX " wg/cu" #WGPC " opt" #OPT " xw" #WE ":" #WO, true, G, \
+            CH, WGPC, OPT,                                                                                     \
             [](dim3 g, hipStream_t s, const uint8_t *b, uint64_t n, uint32_t bs, const uint32_t *img,           \
                const uint32_t *fold, uint32_t *o) {                                                            \
                 hipLaunchKernelGGL((crc_rows_kernel<G, CH, NB, AUX, OPT>), g, dim3(kThreads), 0, s, b, n, bs, img, \
-                                   fold, o);                                                                   \
+                                   fold, o, (uint32_t)(((WE) << 16) | (WO)));                                  \
             }, {}}
+#define CRC_VARIANT(G, CH, NB, AUX, WGPC, OPT) CRC_VARIANT_W(G, CH, NB, AUX, WGPC, OPT, 0, 0)
 #define CRC2_VARIANT(G, CH, NB, AUX, WGPC)                                                                     \
     Variant{"crc2 G" #G " CH" #CH " NBUF" #NB " AUX" #AUX " wg/cu" #WGPC, true, G, CH, WGPC, -1,            \
             [](dim3 g, hipStream_t s, const uint8_t *b, uint64_t n, uint32_t bs, const uint32_t *img,           \
@@ -151,12 +153,15 @@ static uint32_t *g_ctr = nullptr;
                 hipLaunchKernelGGL((crc_rows_dyn_kernel<G, CH, NB, AUX, OPT>), g, dim3(kThreads), 0, s, b, n, bs, \
                                    img, fold, o, g_ctr);                                                       \
             }, {}}
-#define ROOF_VARIANT(G, CH, NB, AUX, WGPC)                                                                 \
-    Variant{"roof G" #G " CH" #CH " NBUF" #NB " AUX" #AUX " wg/cu" #WGPC, false, G, CH, WGPC, -1,         \
+#define ROOF_VARIANT_W(G, CH, NB, AUX, WGPC, WE, WO)                                                        \
+    Variant{"roof G" #G " CH" #CH " NBUF" #NB " AUX" #AUX " wg/cu" #WGPC " xw" #WE ":" #WO, false, G, CH,     \
+            WGPC, -1,                                                                                      \
             [](dim3 g, hipStream_t s, const uint8_t *b, uint64_t n, uint32_t bs, const uint32_t *img,       \
                const uint32_t *fold, uint32_t *o) {                                                        \
-                hipLaunchKernelGGL((roof_rows<G, CH, NB, AUX>), g, dim3(kThreads), 0, s, b, n, bs, img, fold, o); \
+                hipLaunchKernelGGL((roof_rows<G, CH, NB, AUX>), g, dim3(kThreads), 0, s, b, n, bs, img, fold, o, \
+                                   (uint32_t)(((WE) << 16) | (WO)));                                       \
             }, {}}
+#define ROOF_VARIANT(G, CH, NB, AUX, WGPC) ROOF_VARIANT_W(G, CH, NB, AUX, WGPC, 0, 0)
 
 int main(int argc, char **argv)
 {
@@ -193,18 +198,21 @@ int main(int argc, char **argv)
     std::vector<Variant> all;
     // first entry = product reference for the bit-exact cross-check and the sustained run
     all.push_back(CRC_VARIANT(32, 8, 2, 2, 1, 2));
-    all.push_back(CRC_VARIANT(32, 8, 2, 2, 1, 34));
-    all.push_back(CRC_VARIANT(32, 8, 2, 2, 1, 66));
-    all.push_back(CRC_VARIANT(32, 8, 3, 2, 1, 2));
-    all.push_back(CRC_VARIANT(32, 8, 3, 2, 1, 34));
+    all.push_back(CRC_VARIANT_W(32, 8, 2, 2, 1, 2, 41, 39));
+    all.push_back(CRC_VARIANT_W(32, 8, 2, 2, 1, 2, 61, 59));
+    all.push_back(CRC_VARIANT_W(32, 8, 2, 2, 1, 2, 31, 29));
+    all.push_back(CRC_VARIANT_W(32, 8, 3, 2, 1, 2, 41, 39));
     all.push_back(CRC_VARIANT(32, 8, 2, 2, 1, 10));
-    all.push_back(CRC_VARIANT(32, 8, 2, 2, 1, 42));
+    all.push_back(CRC_VARIANT(32, 8, 2, 2, 1, 138));
     all.push_back(CRC_VARIANT(64, 4, 2, 2, 1, 0));
-    all.push_back(CRC_VARIANT(64, 4, 2, 2, 1, 32));
+    all.push_back(CRC_VARIANT_W(64, 4, 2, 2, 1, 0, 41, 39));
+    all.push_back(CRC_VARIANT_W(64, 4, 2, 2, 1, 0, 31, 29));
     all.push_back(CRC_VARIANT(64, 4, 2, 2, 1, 8));
-    all.push_back(CRC_VARIANT(64, 4, 2, 2, 1, 40));
+    all.push_back(CRC_VARIANT(64, 4, 2, 2, 1, 136));
     all.push_back(ROOF_VARIANT(32, 8, 2, 2, 1));
+    all.push_back(ROOF_VARIANT_W(32, 8, 2, 2, 1, 41, 39));
     all.push_back(ROOF_VARIANT(64, 4, 2, 2, 2));
+    all.push_back(ROOF_VARIANT_W(64, 4, 2, 2, 2, 41, 39));
     // EXPLORE_FILTER="a,b,c": keep only variants whose name contains one of the substrings
     std::vector<std::string> filt;
     if (const char *f = getenv("EXPLORE_FILTER")) {
