@@ -67,6 +67,19 @@ int priskv_crc32_ranges_dev(const priskv_crc_ctx *ctx, const void *d_base,
                             const uint64_t *d_offsets, const uint32_t *d_lengths, uint64_t n,
                             uint32_t *d_out, void *stream);
 
+/* Device-side verify of per-value extents (client-side integrity check):
+ * compares priskv_crc32(d_base + d_offsets[i], d_lengths[i]) with
+ * d_expected[i] for every i and writes d_status[0] = the number of values
+ * that differ and d_status[1] = the smallest such i (UINT64_MAX if none).
+ * Replaces copying the whole value pool to the host and memcmp'ing each value
+ * (client/benchmark.c:735-761, pypriskv/testing.py:64-66): only 16 bytes of
+ * status need to leave the device.  d_status is 2 x uint64_t device memory,
+ * written asynchronously on `stream`; d_expected holds the CRCs computed when
+ * the values were written (e.g. by this library on the sending buffer). */
+int priskv_crc32_verify_dev(const priskv_crc_ctx *ctx, const void *d_base, const uint64_t *d_offsets,
+                            const uint32_t *d_lengths, uint64_t n, const uint32_t *d_expected,
+                            uint64_t *d_status, void *stream);
+
 /* Host-resident per-value extents -- the memfile scrub at recovery
  * (server/kv.c:824-875 walks the keys; each live value is valuelen bytes at
  * value_off inside the value region, server/memory.h:50-51).  The kernel
@@ -100,9 +113,34 @@ int priskv_crc32_ranges_host_multi(priskv_crc_ctx *const *ctxs, int nctx, const 
                                    uint64_t region_bytes, const uint64_t *h_offsets,
                                    const uint32_t *h_lengths, uint64_t n, uint32_t *h_out);
 
+/* SET-completion batcher.  PrisKV finishes a SET when the RDMA READ of the
+ * value into its block completes (server/rdma.c:1417-1418 ->
+ * server/kv.c:505), per request on each io thread; a launch per value costs
+ * more than its CRC, so completions are batched here.  io threads submit
+ * (value_off, valuelen, cookie) -- thread-safe and sharded per thread (no
+ * shared lock); it blocks only when 8 * max_batch values are already queued.  A worker thread hashes the queue
+ * when it holds max_batch values or its oldest value has waited
+ * max_delay_us: ONE zero-copy extents pass over h_region (registered at
+ * create unless it already is), then cb(arg, cookie, crc, status) for every
+ * value from the worker thread -- one submitting thread's values in its
+ * submission order -- (status 0, or the pass's -errno with crc 0).  flush blocks until every value submitted
+ * before it has been called back; destroy flushes, stops the worker and
+ * undoes its registration.  The context must outlive the batcher. */
+typedef struct priskv_crc_batch priskv_crc_batch;
+typedef void (*priskv_crc_batch_cb)(void *arg, uint64_t cookie, uint32_t crc, int status);
+int priskv_crc_batch_create(priskv_crc_ctx *ctx, const void *h_region, uint64_t region_bytes,
+                            uint32_t max_batch, uint32_t max_delay_us, priskv_crc_batch_cb cb, void *arg,
+                            priskv_crc_batch **out);
+int priskv_crc_batch_submit(priskv_crc_batch *b, uint64_t value_off, uint32_t valuelen, uint64_t cookie);
+/* n completions at once (one CQ poll's worth): one lock instead of n */
+int priskv_crc_batch_submitv(priskv_crc_batch *b, uint64_t n, const uint64_t *value_offs,
+                             const uint32_t *valuelens, const uint64_t *cookies);
+int priskv_crc_batch_flush(priskv_crc_batch *b);
+void priskv_crc_batch_destroy(priskv_crc_batch *b);
+
 /* Page-lock an existing host range (e.g. the mmap'd memfile value region,
  * server/memory.c:351-457) for direct DMA and zero-copy reads by every GPU
- * (portable + mapped), and undo it. */
+ * (portable + mapped), and undo it.  -EEXIST: the range is already registered. */
 int priskv_crc_host_register(void *h_base, uint64_t len);
 int priskv_crc_host_unregister(void *h_base);
 

@@ -41,6 +41,8 @@ SIGNATURES = [
      [_C.c_void_p, _C.c_void_p, _C.c_uint64, _C.c_uint32, _C.c_void_p, _C.c_void_p]),
     ("priskv_crc32_ranges_dev", _C.c_int,
      [_C.c_void_p, _C.c_void_p, _C.c_void_p, _C.c_void_p, _C.c_uint64, _C.c_void_p, _C.c_void_p]),
+    ("priskv_crc32_verify_dev", _C.c_int,
+     [_C.c_void_p, _C.c_void_p, _C.c_void_p, _C.c_void_p, _C.c_uint64, _C.c_void_p, _C.c_void_p, _C.c_void_p]),
     ("priskv_crc32_blocks_host", _C.c_int,
      [_C.c_void_p, _C.c_void_p, _C.c_uint64, _C.c_uint32, _C.c_void_p]),
     ("priskv_crc32_ranges_host", _C.c_int,
@@ -49,6 +51,13 @@ SIGNATURES = [
      [_C.c_void_p, _C.c_int, _C.c_void_p, _C.c_uint64, _C.c_uint32, _C.c_void_p]),
     ("priskv_crc32_ranges_host_multi", _C.c_int,
      [_C.c_void_p, _C.c_int, _C.c_void_p, _C.c_uint64, _C.c_void_p, _C.c_void_p, _C.c_uint64, _C.c_void_p]),
+    ("priskv_crc_batch_create", _C.c_int,
+     [_C.c_void_p, _C.c_void_p, _C.c_uint64, _C.c_uint32, _C.c_uint32, _C.c_void_p, _C.c_void_p,
+      _C.POINTER(_C.c_void_p)]),
+    ("priskv_crc_batch_submit", _C.c_int, [_C.c_void_p, _C.c_uint64, _C.c_uint32, _C.c_uint64]),
+    ("priskv_crc_batch_submitv", _C.c_int, [_C.c_void_p, _C.c_uint64, _C.c_void_p, _C.c_void_p, _C.c_void_p]),
+    ("priskv_crc_batch_flush", _C.c_int, [_C.c_void_p]),
+    ("priskv_crc_batch_destroy", None, [_C.c_void_p]),
     ("priskv_crc_host_register", _C.c_int, [_C.c_void_p, _C.c_uint64]),
     ("priskv_crc_host_unregister", _C.c_int, [_C.c_void_p]),
     ("priskv_crc32_shift", _C.c_uint32, [_C.c_uint32, _C.c_uint64]),
@@ -188,6 +197,22 @@ class CrcContext:
                "priskv_crc32_ranges_dev")
         return out
 
+    def verify_dev(self, region, offsets, lengths, expected, status=None, stream=None):
+        """Device verify (priskv_crc32_verify_dev): returns the 2-entry int64
+        status tensor {mismatches, first mismatching index or -1 (UINT64_MAX)},
+        filled asynchronously on `stream`."""
+        import torch
+        n = offsets.numel()
+        if (lengths.numel() != n or expected.numel() != n or offsets.dtype != torch.int64
+                or lengths.dtype != torch.int32 or expected.element_size() != 4):
+            raise ValueError("offsets int64, lengths int32 and expected 4-byte device tensors of equal length")
+        if status is None:
+            status = torch.empty(2, dtype=torch.int64, device=region.device)
+        _check(lib().priskv_crc32_verify_dev(self._h, region.data_ptr(), offsets.data_ptr(), lengths.data_ptr(),
+                                             n, expected.data_ptr(), status.data_ptr(), _stream_ptr(stream)),
+               "priskv_crc32_verify_dev")
+        return status
+
     def fill_splitmix(self, region, seed: int, word_offset: int = 0, stream=None, nbytes=None) -> None:
         nb = region.numel() * region.element_size() if nbytes is None else nbytes
         _check(lib().priskv_crc_fill_splitmix_dev(self._h, region.data_ptr(), nb, seed & (2**64 - 1),
@@ -250,6 +275,49 @@ def ranges_host_multi(ctxs, region: np.ndarray, offsets, lengths, out: Optional[
                                                 offs.ctypes.data, lens.ctypes.data, offs.size, out.ctypes.data),
            "priskv_crc32_ranges_host_multi")
     return out
+
+
+BATCH_CB = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int)
+
+
+class CrcBatcher:
+    """SET-completion batcher (priskv_crc_batch_*): submit (value_off,
+    valuelen, cookie) from any thread; callback(cookie, crc, status) runs on
+    the library's worker thread once the value's batch has been hashed."""
+
+    def __init__(self, ctx: "CrcContext", region: np.ndarray, callback, max_batch: int = 1024,
+                 max_delay_us: int = 200):
+        self._region = region  # keep the mapping alive
+        self._cb = BATCH_CB(lambda _arg, cookie, crc, status: callback(cookie, crc, status))
+        self._h = ctypes.c_void_p()
+        _check(lib().priskv_crc_batch_create(ctx.handle, region.ctypes.data, region.nbytes, max_batch, max_delay_us,
+                                             self._cb, None, ctypes.byref(self._h)), "priskv_crc_batch_create")
+
+    def submit(self, value_off: int, valuelen: int, cookie: int) -> None:
+        _check(lib().priskv_crc_batch_submit(self._h, value_off, valuelen, cookie), "priskv_crc_batch_submit")
+
+    def submitv(self, value_offs, valuelens, cookies) -> None:
+        o = np.ascontiguousarray(value_offs, dtype=np.uint64)
+        ln = np.ascontiguousarray(valuelens, dtype=np.uint32)
+        c = np.ascontiguousarray(cookies, dtype=np.uint64)
+        if not (o.size == ln.size == c.size):
+            raise ValueError("value_offs, valuelens and cookies must have the same length")
+        _check(lib().priskv_crc_batch_submitv(self._h, o.size, o.ctypes.data, ln.ctypes.data, c.ctypes.data),
+               "priskv_crc_batch_submitv")
+
+    def flush(self) -> None:
+        _check(lib().priskv_crc_batch_flush(self._h), "priskv_crc_batch_flush")
+
+    def close(self) -> None:
+        if self._h:
+            lib().priskv_crc_batch_destroy(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
 
 
 def as_u32(t) -> np.ndarray:

@@ -102,6 +102,8 @@ inline int herr(hipError_t e)
         return -ENOMEM;
     if (e == hipErrorNoDevice || e == hipErrorInvalidDevice)
         return -ENODEV;
+    if (e == hipErrorHostMemoryAlreadyRegistered)
+        return -EEXIST;
     return -EIO;
 }
 
@@ -513,6 +515,40 @@ int priskv_crc32_ranges_dev(const priskv_crc_ctx *ctx, const void *d_base, const
     if (!g.ok)
         return -ENODEV;
     return launch_extents(ctx, (const uint8_t *)d_base, n, d_offsets, d_lengths, 0, 0, d_out, (hipStream_t)stream);
+}
+
+int priskv_crc32_verify_dev(const priskv_crc_ctx *ctx, const void *d_base, const uint64_t *d_offsets,
+                            const uint32_t *d_lengths, uint64_t n, const uint32_t *d_expected,
+                            uint64_t *d_status, void *stream)
+{
+    if (!ctx || !d_status)
+        return -EINVAL;
+    if (n && (!d_base || !d_offsets || !d_lengths || !d_expected))
+        return -EINVAL;
+    DevGuard g(ctx->device);
+    if (!g.ok)
+        return -ENODEV;
+    hipStream_t s = (hipStream_t)stream;
+    // status first: a zero-length verify still reports {0, UINT64_MAX}
+    if (int rc = herr(hipMemsetAsync(d_status, 0, sizeof(uint64_t), s)))
+        return rc;
+    if (int rc = herr(hipMemsetAsync(d_status + 1, 0xFF, sizeof(uint64_t), s)))
+        return rc;
+    if (n == 0)
+        return 0;
+    uint32_t *got = nullptr; // stream-ordered scratch: concurrent calls never share it
+    if (int rc = herr(hipMallocAsync((void **)&got, n * sizeof(uint32_t), s)))
+        return rc;
+    int rc = launch_extents(ctx, (const uint8_t *)d_base, n, d_offsets, d_lengths, 0, 0, got, s);
+    if (!rc) {
+        const uint64_t want = (n + 255) / 256;
+        const uint32_t grid = (uint32_t)(want < (uint64_t)ctx->num_cus * 4 ? want : (uint64_t)ctx->num_cus * 4);
+        hipLaunchKernelGGL(crc_verify_kernel, dim3(grid), dim3(256), 0, s, got, d_expected, n,
+                           (unsigned long long *)d_status);
+        rc = herr(hipGetLastError());
+    }
+    const int frc = herr(hipFreeAsync(got, s));
+    return rc ? rc : frc;
 }
 
 int priskv_crc_fill_splitmix_dev(const priskv_crc_ctx *ctx, void *d_dst, uint64_t nbytes, uint64_t seed,

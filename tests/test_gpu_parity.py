@@ -233,6 +233,98 @@ def test_segmented_large_blocks(torch_cuda, ctx, bs, nb):
     assert np.array_equal(_u32(out), want), (bs, nb)
 
 
+def test_verify_dev(torch_cuda, ctx):
+    """Device verify: CRC each value where it landed and compare with the
+    expected CRCs (the oracle's); corrupted values are counted and the first
+    one is reported."""
+    torch = torch_cuda
+    n_bytes = 16 << 20
+    t = _region(torch, ctx, n_bytes, SEED, 5)
+    rng = np.random.default_rng(8)
+    k = 5000
+    lens = rng.integers(0, 9000, k).astype(np.uint32)
+    offs = np.array([rng.integers(0, n_bytes - int(ln)) for ln in lens], dtype=np.uint64)
+    want = O.crc32_ranges(t[:n_bytes].cpu().numpy(), offs, lens)
+    d_o = torch.from_numpy(offs.astype(np.int64)).cuda()
+    d_l = torch.from_numpy(lens.view(np.int32)).cuda()
+    d_e = torch.from_numpy(want.view(np.int32)).cuda()
+    st = ctx.verify_dev(t, d_o, d_l, d_e)
+    torch.cuda.synchronize()
+    assert st.cpu().tolist() == [0, -1]
+    # corrupt one byte inside three chosen values (not shared with value 0..9)
+    bad = [4999, 1234, 777]
+    for i in bad:
+        if lens[i] == 0:
+            lens[i] = 1
+    d_l = torch.from_numpy(lens.view(np.int32)).cuda()
+    want = O.crc32_ranges(t[:n_bytes].cpu().numpy(), offs, lens)
+    d_e = torch.from_numpy(want.view(np.int32)).cuda()
+    for i in bad:
+        t[int(offs[i]) + int(lens[i]) // 2] ^= 0x40
+    got = _u32(ctx.ranges_dev(t, d_o, d_l))
+    mism = np.nonzero(got != want)[0]
+    st = ctx.verify_dev(t, d_o, d_l, d_e).cpu().tolist()
+    assert st == [len(mism), int(mism[0])] and set(bad) <= set(mism.tolist())
+    # empty batch
+    e = torch.empty(0, dtype=torch.int64, device="cuda")
+    st = ctx.verify_dev(t, e, e.to(torch.int32), e.to(torch.int32)).cpu().tolist()
+    assert st == [0, -1]
+
+
+def test_set_completion_batcher(torch_cuda, ctx):
+    """SET-completion batcher: 4 submitting threads, every value called back
+    exactly once with the oracle's CRC; the deadline path (no flush); close()
+    drains; out-of-range extents are refused."""
+    import threading
+    import time
+    from priskv_amd import CrcBatcher
+    region = O.fill_splitmix(64 << 20, SEED, 17)
+    rng = np.random.default_rng(23)
+    k = 12000
+    lens = rng.integers(0, 20000, k).astype(np.uint32)
+    offs = np.array([rng.integers(0, region.size - int(ln)) for ln in lens], dtype=np.uint64)
+    want = O.crc32_ranges(region, offs, lens)
+    got, lock = {}, threading.Lock()
+
+    def cb(cookie, crc, status):
+        with lock:
+            assert cookie not in got
+            got[cookie] = (crc, status)
+
+    with CrcBatcher(ctx, region, cb, max_batch=700, max_delay_us=300) as b:
+        def worker(t):
+            if t % 2:  # vectored: a CQ poll's worth of completions per call
+                idx = np.arange(t, k, 4)
+                for c in range(0, idx.size, 16):
+                    j = idx[c:c + 16]
+                    b.submitv(offs[j], lens[j], j)
+            else:
+                for i in range(t, k, 4):
+                    b.submit(int(offs[i]), int(lens[i]), i)
+        th = [threading.Thread(target=worker, args=(t,)) for t in range(4)]
+        for x in th:
+            x.start()
+        for x in th:
+            x.join()
+        b.flush()
+        assert len(got) == k
+        assert all(got[i] == (int(want[i]), 0) for i in range(k))
+        # deadline path: a partial batch is hashed without a flush
+        got.clear()
+        for i in range(3):
+            b.submit(int(offs[i]), int(lens[i]), i)
+        t0 = time.time()
+        while len(got) < 3 and time.time() - t0 < 10:
+            time.sleep(0.001)
+        assert got == {i: (int(want[i]), 0) for i in range(3)}
+        with pytest.raises(OSError):
+            b.submit(region.size - 10, 11, 99)
+        got.clear()
+        for i in range(100):
+            b.submit(int(offs[i]), int(lens[i]), i)
+    assert len(got) == 100  # close() drained the queue
+
+
 def test_ranges_beyond_2GiB_and_many_per_wave(torch_cuda, ctx):
     """Extents at offsets with bit 31 (and bit 32) set, and far more extents
     than waves so each wave loops over many of them (a sign-extension of the

@@ -31,6 +31,7 @@ def _declared_functions():
         src = open(os.path.join(INCLUDE, h)).read()
         src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
         src = re.sub(r"//.*", "", src)
+        src = re.sub(r"typedef[^;]*;", "", src)
         for m in re.finditer(r"\b([A-Za-z_][A-Za-z0-9_]*)\s*\([^;{]*\)\s*;", src):
             names.add(m.group(1))
     return names
@@ -51,6 +52,9 @@ def test_library_exports_nothing_else():
                          check=True).stdout
     exported = {ln.split()[-1] for ln in out.splitlines() if " T " in ln}
     assert exported == _declared_functions(), exported ^ _declared_functions()
+    # no weak C++ template / class symbols leak either (the batcher is C++)
+    weak = [ln.split()[-1] for ln in out.splitlines() if " W " in ln or " V " in ln]
+    assert not [w for w in weak if w.startswith("_Z")], weak
 
 
 def test_version():
@@ -155,6 +159,14 @@ def test_batch_entry_points_reject_bad_args_without_gpu():
     # NULL context is rejected before any HIP call
     assert L.priskv_crc32_blocks_dev(None, 1, 1, 4096, 1, None) == -22
     assert L.priskv_crc32_ranges_dev(None, 1, 1, 1, 1, 1, None) == -22
+    assert L.priskv_crc32_verify_dev(None, 1, 1, 1, 1, 1, 16, None) == -22
+    h = ctypes.c_void_p()
+    cb = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int)(lambda *a: None)
+    assert L.priskv_crc_batch_create(None, 16, 4096, 64, 100, cb, None, ctypes.byref(h)) == -22
+    assert L.priskv_crc_batch_submit(None, 0, 16, 0) == -22
+    assert L.priskv_crc_batch_submitv(None, 0, None, None, None) == -22
+    assert L.priskv_crc_batch_flush(None) == -22
+    L.priskv_crc_batch_destroy(None)  # no-op
     assert L.priskv_crc32_blocks_host(None, 1, 1, 4096, 1) == -22
     assert L.priskv_crc_fill_splitmix_dev(None, 16, 16, 0, 0, None) == -22
     assert L.priskv_crc32_blocks_path(None, 1, 4096) == -22
@@ -196,7 +208,8 @@ def test_library_is_not_stale():
     csrc = os.path.join(ROOT, "priskv_amd", "csrc")
     headers = [os.path.join(INCLUDE, f) for f in os.listdir(INCLUDE)] + [os.path.join(csrc, "crc_internal.h")]
     deps = {
-        "libpriskv_crc.so": headers + [os.path.join(csrc, f) for f in ("crc_gpu.hip", "crc_device.inc", "crc_host.c")],
+        "libpriskv_crc.so": headers + [os.path.join(csrc, f)
+                                       for f in ("crc_gpu.hip", "crc_device.inc", "crc_host.c", "crc_batch.cpp")],
         "libpriskv_crc_host.a": headers + [os.path.join(csrc, "crc_host.c")],
     }
     for lib, srcs in deps.items():
