@@ -166,4 +166,44 @@ double oracle_time_blocks_fn(crc_fn fn, const uint8_t *base, uint64_t nblocks, u
     return (double)(b.tv_sec - a.tv_sec) + 1e-9 * (double)(b.tv_nsec - a.tv_nsec);
 }
 
+/* the same pass split over nthreads (static contiguous block ranges, the
+ * SURVEY 8(d) "nproc threads" CPU reference); returns wall seconds */
+struct time_mt_arg {
+    crc_fn fn;
+    const uint8_t *base;
+    uint64_t lo, hi;
+    uint32_t bs;
+    uint32_t *out;
+};
+
+static void *time_mt_worker(void *p)
+{
+    struct time_mt_arg *a = (struct time_mt_arg *)p;
+    for (uint64_t i = a->lo; i < a->hi; i++)
+        a->out[i] = a->fn((uint8_t *)a->base + i * (uint64_t)a->bs, a->bs);
+    return NULL;
+}
+
+double oracle_time_blocks_fn_mt(crc_fn fn, const uint8_t *base, uint64_t nblocks, uint32_t block_size,
+                                uint32_t *out, int nthreads)
+{
+    if (nthreads < 1)
+        nthreads = 1;
+    if (nthreads > 256)
+        nthreads = 256;
+    pthread_t th[256];
+    struct time_mt_arg args[256];
+    struct timespec a, b;
+    clock_gettime(CLOCK_MONOTONIC, &a);
+    for (int t = 0; t < nthreads; t++) {
+        args[t] = (struct time_mt_arg){fn, base, nblocks * (uint64_t)t / (uint64_t)nthreads,
+                                       nblocks * (uint64_t)(t + 1) / (uint64_t)nthreads, block_size, out};
+        pthread_create(&th[t], NULL, time_mt_worker, &args[t]);
+    }
+    for (int t = 0; t < nthreads; t++)
+        pthread_join(th[t], NULL);
+    clock_gettime(CLOCK_MONOTONIC, &b);
+    return (double)(b.tv_sec - a.tv_sec) + 1e-9 * (double)(b.tv_nsec - a.tv_nsec);
+}
+
 uint32_t oracle_crc32_u32len(uint8_t *buf, uint32_t len) { return oracle_crc32(buf, len); }

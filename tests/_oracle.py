@@ -142,8 +142,8 @@ def splitmix_numpy(nwords: int, seed: int, word_offset: int = 0) -> np.ndarray:
     return z
 
 
-def time_cpu_baseline(region: np.ndarray, block_size: int, prefer: str = "reference"):
-    """Time a single-threaded CPU pass over region's blocks in C.
+def time_cpu_baseline(region: np.ndarray, block_size: int, prefer: str = "reference", threads: int = 1):
+    """Time a CPU pass over region's blocks in C (threads > 1: static split).
 
     prefer="reference": the reference's own server/crc.c (oracle/_ref, -O2,
     its release flag) when it was built; otherwise our restatement ("port").
@@ -162,5 +162,11 @@ def time_cpu_baseline(region: np.ndarray, block_size: int, prefer: str = "refere
     else:
         fn = ctypes.cast(L.oracle_crc32_u32len, ctypes.c_void_p).value
         kind, label = "port", "oracle/crc_oracle.c byte-serial restatement -O2"
-    secs = L.oracle_time_blocks_fn(fn, region.ctypes.data, n, block_size, out.ctypes.data)
+    if threads > 1:
+        L.oracle_time_blocks_fn_mt.restype = ctypes.c_double
+        L.oracle_time_blocks_fn_mt.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32,
+                                               ctypes.c_void_p, ctypes.c_int]
+        secs = L.oracle_time_blocks_fn_mt(fn, region.ctypes.data, n, block_size, out.ctypes.data, threads)
+    else:
+        secs = L.oracle_time_blocks_fn(fn, region.ctypes.data, n, block_size, out.ctypes.data)
     return secs, out, kind, label

@@ -128,8 +128,48 @@ def blocks_host_case(ctx, bs=4096, total=2 << 30):
          pageable_GiBs=round(res["pageable"], 2), checked=65536, bit_exact=bool(ok))
 
 
+def memfile_case(ctx, bs=4096, total=2 << 30):
+    """The memfile as the server maps it: a tmpfs file mapped MAP_SHARED
+    (server/memory.c:351-457), registered once with hipHostRegister, then
+    block-streamed and scrubbed per value zero-copy."""
+    import mmap
+    path = f"/dev/shm/priskv_crc_memfile_{os.getpid()}"
+    try:
+        with open(path, "w+b") as f:
+            f.truncate(total)
+            mm = mmap.mmap(f.fileno(), total, flags=mmap.MAP_SHARED, prot=mmap.PROT_READ | mmap.PROT_WRITE)
+        host = np.frombuffer(mm, dtype=np.uint8)
+        host[:] = O.fill_splitmix(total, SEED, 0)
+        host_register(host)
+        try:
+            ctx.blocks_host(host, bs)
+            t0 = time.perf_counter()
+            for _ in range(3):
+                got = ctx.blocks_host(host, bs)
+            blk = total / ((time.perf_counter() - t0) / 3) / 2**30
+            rng = np.random.default_rng(3)
+            offs, lens = extents(rng, 1 << 17, total, bs)
+            ctx.ranges_host(host, offs, lens)
+            t0 = time.perf_counter()
+            for _ in range(3):
+                gr = ctx.ranges_host(host, offs, lens)
+            sec = (time.perf_counter() - t0) / 3
+        finally:
+            host_unregister(host)
+        ok = (np.array_equal(got[:65536], O.crc32_blocks(host[: 65536 * bs], bs, nthreads=16))
+              and np.array_equal(gr[:5000], O.crc32_ranges(host, offs[:5000], lens[:5000])))
+        vb = int(lens.astype(np.uint64).sum())
+        emit(path="memfile_tmpfs_registered", bytes=total, blocks_host_GiBs=round(blk, 2),
+             ranges_host_values=int(offs.size), ranges_host_GiBs=round(vb / sec / 2**30, 2), bit_exact=bool(ok))
+        del host, got, gr
+        mm.close()
+    finally:
+        if os.path.exists(path):
+            os.unlink(path)
+
+
 def main():
-    which = sys.argv[1:] or ["blocks", "ranges", "host"]
+    which = sys.argv[1:] or ["blocks", "ranges", "host", "memfile"]
     ctx = CrcContext(0)
     if "blocks" in which:
         for bs in (16, 64, 256, 512, 1024, 2048, 3072, 4096, 8192, 16384, 20480, 65536, 1 << 20, 100, 4100):
@@ -142,6 +182,8 @@ def main():
     if "host" in which:
         ranges_host_case(ctx)
         blocks_host_case(ctx)
+    if "memfile" in which:
+        memfile_case(ctx)
 
 
 if __name__ == "__main__":

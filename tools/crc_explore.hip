@@ -104,6 +104,24 @@ __global__ __launch_bounds__(256) void roof_gridstride(const v4u *__restrict__ p
     }
     out[(uint64_t)blockIdx.x * blockDim.x + threadIdx.x] = acc;
 }
+// STREAM-style copy ("a measured device STREAM-copy peak"):
+// nt loads and nt stores, grid-stride over 16-B elements
+__global__ __launch_bounds__(256) void copy_gridstride(const v4u *__restrict__ src, v4u *__restrict__ dst,
+                                                       uint64_t n16)
+{
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    for (; i + 3 * stride < n16; i += 4 * stride) {
+        const v4u a = __builtin_nontemporal_load(src + i), b = __builtin_nontemporal_load(src + i + stride),
+                  c = __builtin_nontemporal_load(src + i + 2 * stride), d = __builtin_nontemporal_load(src + i + 3 * stride);
+        __builtin_nontemporal_store(a, dst + i);
+        __builtin_nontemporal_store(b, dst + i + stride);
+        __builtin_nontemporal_store(c, dst + i + 2 * stride);
+        __builtin_nontemporal_store(d, dst + i + 3 * stride);
+    }
+    for (; i < n16; i += stride)
+        dst[i] = src[i];
+}
 } // namespace
 
 #define CK(x)                                                                                      \
@@ -319,6 +337,26 @@ int main(int argc, char **argv)
         }
         std::sort(t.begin(), t.end());
         printf("\n  min %.4f  median %.4f  max %.4f ms\n", t[0], t[n / 2], t[n - 1]);
+    }
+    // STREAM copy of half the buffer onto the other half (read + write bytes)
+    {
+        const uint64_t half16 = (uint64_t)bs * nb / 32;
+        std::vector<float> t;
+        for (int r = 0; r < 12; r++) {
+            CK(hipEventRecord(e0, 0));
+            hipLaunchKernelGGL(copy_gridstride, dim3(ncu * 8), dim3(256), 0, 0, (const v4u *)d,
+                               (v4u *)d + half16, half16);
+            CK(hipEventRecord(e1, 0));
+            CK(hipEventSynchronize(e1));
+            float ms;
+            CK(hipEventElapsedTime(&ms, e0, e1));
+            if (r > 1)
+                t.push_back(ms);
+        }
+        std::sort(t.begin(), t.end());
+        const double moved = 2.0 * (double)half16 * 16;
+        printf("stream copy nt (read+write)              median %8.4f ms  %7.1f GB/s (best %7.1f)\n", t[t.size() / 2],
+               moved / t[t.size() / 2] / 1e6, moved / t[0] / 1e6);
     }
     // per-wave start / end spread of the timing variants (OPT bit 3)
     for (auto &v : V) {
