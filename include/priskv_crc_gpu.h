@@ -151,6 +151,13 @@ int priskv_crc_host_unregister(void *h_base);
 uint32_t priskv_crc32_shift(uint32_t crc, uint64_t nbytes);
 uint32_t priskv_crc32_combine(uint32_t crc_a, uint32_t crc_b, uint64_t len_b);
 
+/* Which host path priskv_crc32 (include/crc.h) folds long inputs with:
+ * "vclmul" (VPCLMULQDQ + AVX-512, inputs >= 256 B), "clmul" (PCLMULQDQ,
+ * >= 64 B) or "slice8" (tables only).  Chosen once from cpuid; the
+ * environment variable PRISKV_CRC_HOST_IMPL=slice8|clmul|vclmul caps it.
+ * Shorter inputs always take the slice-by-8 tables.  Diagnostics. */
+const char *priskv_crc32_host_impl(void);
+
 /* Deterministic test pattern on the device (benchmarks and parity tests):
  * 64-bit little-endian word i of the region = splitmix64 output
  * mix64(seed + (word_offset + i + 1) * 0x9E3779B97F4A7C15).  Asynchronous. */

@@ -62,6 +62,7 @@ SIGNATURES = [
     ("priskv_crc_host_unregister", _C.c_int, [_C.c_void_p]),
     ("priskv_crc32_shift", _C.c_uint32, [_C.c_uint32, _C.c_uint64]),
     ("priskv_crc32_combine", _C.c_uint32, [_C.c_uint32, _C.c_uint32, _C.c_uint64]),
+    ("priskv_crc32_host_impl", _C.c_char_p, []),
     ("priskv_crc_fill_splitmix_dev", _C.c_int,
      [_C.c_void_p, _C.c_void_p, _C.c_uint64, _C.c_uint64, _C.c_uint64, _C.c_void_p]),
     ("priskv_crc32_blocks_path", _C.c_int, [_C.c_void_p, _C.c_uint64, _C.c_uint32]),
@@ -117,6 +118,11 @@ def blocks_path(ptr: int, nblocks: int, block_size: int) -> str:
 
 def version() -> str:
     return lib().priskv_crc_version().decode()
+
+
+def host_impl() -> str:
+    """Host path priskv_crc32 folds long inputs with: vclmul / clmul / slice8."""
+    return lib().priskv_crc32_host_impl().decode()
 
 
 def host_register(arr: np.ndarray) -> None:

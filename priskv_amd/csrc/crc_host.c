@@ -5,7 +5,8 @@
  *    Bit-exact with the reference (reflected 0xEDB88320, init 0 at :92, no
  *    final xor at :108) but processes 8 bytes per step with eight tables
  *    (slice-by-8) instead of the reference's byte-serial table walk
- *    (:70-88).  Reentrant: the tables are built once under pthread_once
+ *    (:70-88), and folds inputs of >= 64 B with carry-less multiplies
+ *    (crc_host_clmul.c: PCLMULQDQ, or VPCLMULQDQ/AVX-512 from 256 B).  Reentrant: the tables are built once under pthread_once
  *    (SURVEY §8b threading row) and only read afterwards; buf is never
  *    written or retained.  It stays on the CPU because its callers hash keys
  *    of <= 1 KiB synchronously on the RDMA completion path
@@ -23,6 +24,7 @@
  */
 #include <pthread.h>
 #include <stdint.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include "../../include/crc.h"
@@ -34,6 +36,10 @@
 static uint32_t g_slice[8][256];     /* g_slice[k][b]: byte b followed by k zero bytes */
 static uint32_t g_zpow[64][32];      /* columns of Z_(2^k) */
 static pthread_once_t g_once = PTHREAD_ONCE_INIT;
+/* host path of priskv_crc32 for inputs long enough to fold (crc_host_clmul.c);
+ * picked once from cpuid, capped by PRISKV_CRC_HOST_IMPL=slice8|clmul|vclmul */
+enum { IMPL_SLICE8, IMPL_CLMUL, IMPL_VCLMUL };
+static int g_impl = IMPL_SLICE8;
 
 static uint32_t mat_apply(const uint32_t m[32], uint32_t v)
 {
@@ -73,6 +79,20 @@ static void host_init(void)
     }
     for (int k = 1; k < 64; k++)
         mat_compose(g_zpow[k], g_zpow[k - 1], g_zpow[k - 1]);
+#if defined(__x86_64__)
+    prv_clmul_init();
+    __builtin_cpu_init();
+    if (__builtin_cpu_supports("pclmul"))
+        g_impl = IMPL_CLMUL;
+    if (g_impl == IMPL_CLMUL && __builtin_cpu_supports("avx512f") && __builtin_cpu_supports("vpclmulqdq"))
+        g_impl = IMPL_VCLMUL;
+    const char *want = getenv("PRISKV_CRC_HOST_IMPL");
+    if (want) {
+        const int cap = !strcmp(want, "slice8") ? IMPL_SLICE8 : (!strcmp(want, "clmul") ? IMPL_CLMUL : IMPL_VCLMUL);
+        if (cap < g_impl)
+            g_impl = cap;
+    }
+#endif
 }
 
 static inline uint32_t load_le32(const uint8_t *p)
@@ -82,11 +102,9 @@ static inline uint32_t load_le32(const uint8_t *p)
     return v; /* x86-64 / aarch64-le hosts */
 }
 
-uint32_t priskv_crc32(uint8_t *buf, uint32_t len)
+/* slice-by-8 over whole 8-byte steps, then byte steps (server/crc.c:70-73) */
+uint32_t prv_crc32_table(uint32_t crc, const uint8_t *p, uint64_t len)
 {
-    pthread_once(&g_once, host_init);
-    uint32_t crc = 0;
-    const uint8_t *p = buf;
     while (len >= 8) {
         uint32_t lo = load_le32(p) ^ crc;
         uint32_t hi = load_le32(p + 4);
@@ -99,6 +117,25 @@ uint32_t priskv_crc32(uint8_t *buf, uint32_t len)
     while (len--)
         crc = g_slice[0][(crc ^ *p++) & 0xff] ^ (crc >> 8);
     return crc;
+}
+
+uint32_t priskv_crc32(uint8_t *buf, uint32_t len)
+{
+    pthread_once(&g_once, host_init);
+#if defined(__x86_64__)
+    if (len >= 256 && g_impl >= IMPL_VCLMUL)
+        return prv_crc32_vclmul(0, buf, len);
+    if (len >= 64 && g_impl >= IMPL_CLMUL)
+        return prv_crc32_clmul(0, buf, len);
+#endif
+    return prv_crc32_table(0, buf, len);
+}
+
+const char *priskv_crc32_host_impl(void)
+{
+    pthread_once(&g_once, host_init);
+    static const char *const names[] = {"slice8", "clmul", "vclmul"};
+    return names[g_impl];
 }
 
 uint32_t priskv_crc32_shift(uint32_t crc, uint64_t nbytes)

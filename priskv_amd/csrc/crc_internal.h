@@ -24,6 +24,12 @@ PRV_HIDDEN void prv_lds_image(uint32_t out[PRV_LDS_WORDS], uint32_t gap_bytes);
 PRV_HIDDEN void prv_fold_columns(uint32_t out[32 * 64], uint32_t group);
 PRV_HIDDEN void prv_shift_columns(uint32_t out[32], uint64_t nbytes);
 PRV_HIDDEN void prv_sarwate_table(uint32_t out[256]);
+/* host CRC register update (init = crc, no xor): tables; clmul folding for
+ * len >= 64 / vclmul for len >= 256 (x86-64, after prv_clmul_init) */
+PRV_HIDDEN uint32_t prv_crc32_table(uint32_t crc, const uint8_t *p, uint64_t len);
+PRV_HIDDEN void prv_clmul_init(void);
+PRV_HIDDEN uint32_t prv_crc32_clmul(uint32_t crc, const uint8_t *p, uint64_t len);
+PRV_HIDDEN uint32_t prv_crc32_vclmul(uint32_t crc, const uint8_t *p, uint64_t len);
 /* out[p*32 + i] = column i of Z_-p (p = 0..15): undoes p trailing zero bytes */
 PRV_HIDDEN void prv_unshift_columns(uint32_t out[16 * 32]);
 

@@ -1,8 +1,9 @@
 """CPU-side checks of the product library (no GPU needed).
 
 * libpriskv_crc.so loads and exports exactly the functions include/*.h declare;
-* priskv_crc32 (the drop-in for server/crc.h:37, host slice-by-8) is bit-exact
-  with the golden vectors and the oracle;
+* priskv_crc32 (the drop-in for server/crc.h:37: host slice-by-8, PCLMULQDQ
+  and VPCLMULQDQ folding) is bit-exact with the golden vectors and the oracle
+  on every host path;
 * the static drop-in archive links into a C program written against
   include/crc.h the way server/kv.c calls it (server/kv.c:314);
 * GF(2) shift/combine identities the GPU fold relies on.
@@ -86,6 +87,41 @@ def test_priskv_crc32_vs_oracle_unaligned():
         n = int(rng.integers(0, 4000))
         s = buf[off:off + n]
         assert C.priskv_crc32(s) == O.crc32(s)
+
+
+_IMPL_CHECK = r"""
+import sys, numpy as np
+sys.path[:0] = [{root!r}, {tests!r}]
+import _oracle as O
+from priskv_amd import crc as C
+print(C.host_impl())
+rng = np.random.default_rng(11)
+buf = rng.integers(0, 256, 70000, dtype=np.uint8)
+# every length around the fold thresholds (64, 256) and lane multiples, then
+# random lengths up to 64 KiB, at every alignment mod 64
+lens = list(range(0, 1100)) + [int(n) for n in rng.integers(0, 65536, 200)]
+for i, n in enumerate(lens):
+    off = i % 64
+    s = buf[off:off + n]
+    assert C.priskv_crc32(s) == O.crc32(s), (n, off)
+print("ok")
+"""
+
+
+@pytest.mark.parametrize("impl", ["slice8", "clmul", "vclmul"])
+def test_priskv_crc32_every_host_path(impl):
+    # the path is fixed once per process (cpuid, capped by the environment):
+    # one child process per path
+    code = _IMPL_CHECK.format(root=ROOT, tests=os.path.join(ROOT, "tests"))
+    env = dict(os.environ, PRISKV_CRC_HOST_IMPL=impl)
+    r = subprocess.run([os.sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    got_impl, status = r.stdout.split()
+    assert status == "ok"
+    order = ["slice8", "clmul", "vclmul"]
+    assert order.index(got_impl) <= order.index(impl)  # capped, never raised
+    if got_impl != impl:
+        pytest.skip(f"this CPU lacks the {impl} instructions (ran {got_impl})")
 
 
 def test_priskv_crc32_threads():
@@ -209,8 +245,9 @@ def test_library_is_not_stale():
     headers = [os.path.join(INCLUDE, f) for f in os.listdir(INCLUDE)] + [os.path.join(csrc, "crc_internal.h")]
     deps = {
         "libpriskv_crc.so": headers + [os.path.join(csrc, f)
-                                       for f in ("crc_gpu.hip", "crc_device.inc", "crc_host.c", "crc_batch.cpp")],
-        "libpriskv_crc_host.a": headers + [os.path.join(csrc, "crc_host.c")],
+                                       for f in ("crc_gpu.hip", "crc_device.inc", "crc_host.c", "crc_host_clmul.c",
+                                                 "crc_batch.cpp")],
+        "libpriskv_crc_host.a": headers + [os.path.join(csrc, f) for f in ("crc_host.c", "crc_host_clmul.c")],
     }
     for lib, srcs in deps.items():
         newest = max(os.path.getmtime(p) for p in srcs)

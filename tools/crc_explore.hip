@@ -171,6 +171,21 @@ static uint32_t *g_ctr = nullptr;
                 hipLaunchKernelGGL((crc_rows_dyn_kernel<G, CH, NB, AUX, OPT>), g, dim3(kThreads), 0, s, b, n, bs, \
                                    img, fold, o, g_ctr);                                                       \
             }, {}}
+// paired (forward / backward wave pairs; NEGATIVE RESULT, explorer only --
+// profiles/r01/explore_4k_pair.log: per-XCD finish times equalize, but both
+// the CRC and the read roof lose 2-4 %): slots + epoch via globals
+static uint64_t *g_slots = nullptr;
+static uint32_t g_epoch = 0;
+#define PAIR_VARIANT(G, CH, NB, AUX, WGPC, OPT)                                                                \
+    Variant{((OPT) & 64 ? "roof pair G" #G " CH" #CH " NBUF" #NB " wg/cu" #WGPC                                \
+                        : "crc pair G" #G " CH" #CH " NBUF" #NB " wg/cu" #WGPC " opt" #OPT),                    \
+            !((OPT) & 64), G, CH, WGPC, (OPT) & 64 ? -1 : (OPT),                                               \
+            [](dim3 g, hipStream_t s, const uint8_t *b, uint64_t n, uint32_t bs, const uint32_t *img,           \
+               const uint32_t *fold, uint32_t *o) {                                                            \
+                g.x += g.x & 1;                                                                                \
+                hipLaunchKernelGGL((crc_rows_pair_kernel<G, CH, NB, AUX, OPT>), g, dim3(kThreads), 0, s, b, n, bs, \
+                                   img, fold, o, g_slots, ++g_epoch);                                          \
+            }, {}}
 #define ROOF_VARIANT_W(G, CH, NB, AUX, WGPC, WE, WO)                                                        \
     Variant{"roof G" #G " CH" #CH " NBUF" #NB " AUX" #AUX " wg/cu" #WGPC " xw" #WE ":" #WO, false, G, CH,     \
             WGPC, -1,                                                                                      \
@@ -213,9 +228,17 @@ int main(int argc, char **argv)
     CK(hipDeviceSynchronize());
 
     CK(hipMalloc(&g_ctr, 64));
+    CK(hipMalloc(&g_slots, (size_t)ncu * 2 * kWaves * 128));
+    CK(hipMemset(g_slots, 0, (size_t)ncu * 2 * kWaves * 128));
     std::vector<Variant> all;
     // first entry = product reference for the bit-exact cross-check and the sustained run
     all.push_back(CRC_VARIANT(32, 8, 2, 2, 1, 2));
+    all.push_back(PAIR_VARIANT(32, 8, 2, 2, 1, 2));
+    all.push_back(PAIR_VARIANT(32, 8, 2, 2, 1, 10));
+    all.push_back(PAIR_VARIANT(32, 8, 2, 2, 1, 66));
+    all.push_back(PAIR_VARIANT(64, 4, 2, 2, 1, 0));
+    all.push_back(PAIR_VARIANT(64, 4, 2, 2, 1, 8));
+    all.push_back(PAIR_VARIANT(64, 4, 2, 2, 1, 64));
     all.push_back(CRC_VARIANT_W(32, 8, 2, 2, 1, 2, 41, 39));
     all.push_back(CRC_VARIANT_W(32, 8, 2, 2, 1, 2, 61, 59));
     all.push_back(CRC_VARIANT_W(32, 8, 2, 2, 1, 2, 31, 29));

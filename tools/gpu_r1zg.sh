@@ -1,0 +1,10 @@
+set -e
+R=$GRAFT_REPO_ROOT
+O=$R/gpurun_out/r1zg
+mkdir -p $O
+cd /tmp && export TMPDIR=/tmp && cd $R
+timeout -k 10 600 python -u -m pytest tests -x -v -m gpu --timeout 300 --timeout-method thread > $O/pytest.log 2>&1
+timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1
+timeout -k 10 300 python bench.py > $O/bench.log 2>&1
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof -o run -- python3 bench.py > $O/bench_prof.log 2>&1
+echo ALLDONE
