@@ -23,6 +23,7 @@
 namespace {
 #include "../priskv_amd/csrc/crc_device.inc"
 #include "crc_dyn_explore.inc"
+#include "crc_pair_explore.inc"
 
 // read-only roof with the rows kernel's loop and addressing (same loads, no hashing)
 template <int G, int CH, int NBUF, int AUX>
