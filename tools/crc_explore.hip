@@ -178,7 +178,7 @@ static uint32_t *g_ctr = nullptr;
 static uint64_t *g_slots = nullptr;
 static uint32_t g_epoch = 0;
 #define PAIR_VARIANT(G, CH, NB, AUX, WGPC, OPT)                                                                \
-    Variant{((OPT) & 64 ? "roof pair G" #G " CH" #CH " NBUF" #NB " wg/cu" #WGPC                                \
+    Variant{((OPT) & 64 ? "roof pair G" #G " CH" #CH " NBUF" #NB " wg/cu" #WGPC " opt" #OPT                   \
                         : "crc pair G" #G " CH" #CH " NBUF" #NB " wg/cu" #WGPC " opt" #OPT),                    \
             !((OPT) & 64), G, CH, WGPC, (OPT) & 64 ? -1 : (OPT),                                               \
             [](dim3 g, hipStream_t s, const uint8_t *b, uint64_t n, uint32_t bs, const uint32_t *img,           \
@@ -237,10 +237,21 @@ int main(int argc, char **argv)
     all.push_back(PAIR_VARIANT(32, 8, 2, 2, 1, 2));
     all.push_back(PAIR_VARIANT(32, 8, 2, 2, 1, 10));
     all.push_back(PAIR_VARIANT(32, 8, 2, 2, 1, 66));
+    all.push_back(PAIR_VARIANT(32, 8, 2, 2, 1, 194));
+    all.push_back(PAIR_VARIANT(32, 8, 2, 2, 1, 322));
+    all.push_back(PAIR_VARIANT(32, 8, 2, 2, 1, 258));
     all.push_back(PAIR_VARIANT(64, 4, 2, 2, 1, 0));
     all.push_back(PAIR_VARIANT(64, 4, 2, 2, 1, 8));
     all.push_back(PAIR_VARIANT(64, 4, 2, 2, 1, 64));
     all.push_back(CRC_VARIANT_W(32, 8, 2, 2, 1, 2, 41, 39));
+    all.push_back(CRC_VARIANT_W(32, 8, 2, 2, 1, 2, 33, 27));
+    all.push_back(CRC_VARIANT_W(32, 8, 2, 2, 1, 2, 17, 13));
+    all.push_back(CRC_VARIANT_W(32, 8, 2, 2, 1, 2, 9, 7));
+    all.push_back(CRC_VARIANT_W(32, 8, 2, 2, 1, 10, 31, 29));
+    all.push_back(CRC_VARIANT_W(32, 8, 2, 2, 1, 10, 17, 13));
+    all.push_back(CRC_VARIANT_W(64, 4, 2, 2, 1, 0, 17, 13));
+    all.push_back(CRC_VARIANT_W(64, 4, 2, 2, 1, 8, 31, 29));
+    all.push_back(CRC_VARIANT_W(64, 4, 2, 2, 1, 8, 17, 13));
     all.push_back(CRC_VARIANT_W(32, 8, 2, 2, 1, 2, 61, 59));
     all.push_back(CRC_VARIANT_W(32, 8, 2, 2, 1, 2, 31, 29));
     all.push_back(CRC_VARIANT_W(32, 8, 3, 2, 1, 2, 41, 39));
