@@ -153,6 +153,25 @@ struct Variant {
                                    fold, o, (uint32_t)(((WE) << 16) | (WO)));                                  \
             }, {}}
 #define CRC_VARIANT(G, CH, NB, AUX, WGPC, OPT) CRC_VARIANT_W(G, CH, NB, AUX, WGPC, OPT, 0, 0)
+// oversubscribed: K workgroups per CU in the grid, 32 KiB of dynamic LDS on
+// top of the 64 KiB tables so only ONE is resident per CU -- the hardware
+// dispatcher then hands each CU its next workgroup as it frees up (dynamic
+// balancing within an XCD with no atomics; workgroup b still goes to XCD b % 8)
+#define CRC_VARIANT_OS(G, CH, NB, AUX, K, OPT, WE, WO)                                                        \
+    Variant{"crc G" #G " CH" #CH " NBUF" #NB " AUX" #AUX " oversub" #K " opt" #OPT " xw" #WE ":" #WO, true, G, \
+            CH, K, OPT,                                                                                        \
+            [](dim3 g, hipStream_t s, const uint8_t *b, uint64_t n, uint32_t bs, const uint32_t *img,           \
+               const uint32_t *fold, uint32_t *o) {                                                            \
+                hipLaunchKernelGGL((crc_rows_kernel<G, CH, NB, AUX, OPT>), g, dim3(kThreads), 32768, s, b, n, bs,  \
+                                   img, fold, o, (uint32_t)(((WE) << 16) | (WO)));                             \
+            }, {}}
+#define ROOF_VARIANT_OS(G, CH, NB, AUX, K)                                                                    \
+    Variant{"roof G" #G " CH" #CH " NBUF" #NB " AUX" #AUX " oversub" #K, false, G, CH, K, -1,                 \
+            [](dim3 g, hipStream_t s, const uint8_t *b, uint64_t n, uint32_t bs, const uint32_t *img,           \
+               const uint32_t *fold, uint32_t *o) {                                                            \
+                hipLaunchKernelGGL((roof_rows<G, CH, NB, AUX>), g, dim3(kThreads), 98304, s, b, n, bs, img, fold, \
+                                   o, 0u);                                                                     \
+            }, {}}
 #define CRC2_VARIANT(G, CH, NB, AUX, WGPC)                                                                     \
     Variant{"crc2 G" #G " CH" #CH " NBUF" #NB " AUX" #AUX " wg/cu" #WGPC, true, G, CH, WGPC, -1,            \
             [](dim3 g, hipStream_t s, const uint8_t *b, uint64_t n, uint32_t bs, const uint32_t *img,           \
@@ -244,6 +263,23 @@ int main(int argc, char **argv)
     all.push_back(PAIR_VARIANT(64, 4, 2, 2, 1, 8));
     all.push_back(PAIR_VARIANT(64, 4, 2, 2, 1, 64));
     all.push_back(CRC_VARIANT_W(32, 8, 2, 2, 1, 2, 41, 39));
+    all.push_back(CRC_VARIANT_OS(32, 8, 2, 2, 2, 2, 0, 0));
+    all.push_back(CRC_VARIANT_OS(32, 8, 2, 2, 2, 2, 31, 29));
+    all.push_back(CRC_VARIANT_OS(32, 8, 2, 2, 3, 2, 0, 0));
+    all.push_back(CRC_VARIANT_OS(32, 8, 2, 2, 3, 2, 31, 29));
+    all.push_back(CRC_VARIANT_OS(64, 4, 2, 2, 2, 0, 0, 0));
+    all.push_back(CRC_VARIANT_OS(64, 4, 2, 2, 2, 0, 31, 29));
+    all.push_back(CRC_VARIANT_OS(64, 4, 2, 2, 3, 0, 31, 29));
+    all.push_back(CRC_VARIANT_OS(32, 8, 2, 2, 4, 2, 0, 0));
+    all.push_back(CRC_VARIANT_OS(32, 8, 2, 2, 8, 2, 0, 0));
+    all.push_back(CRC_VARIANT_OS(32, 8, 2, 2, 16, 2, 0, 0));
+    all.push_back(CRC_VARIANT_OS(32, 8, 2, 2, 4, 2, 31, 29));
+    all.push_back(CRC_VARIANT_OS(32, 8, 2, 2, 8, 2, 31, 29));
+    all.push_back(CRC_VARIANT_OS(32, 8, 2, 2, 4, 10, 0, 0));
+    all.push_back(CRC_VARIANT_OS(64, 4, 2, 2, 4, 0, 0, 0));
+    all.push_back(CRC_VARIANT_OS(64, 4, 2, 2, 8, 0, 0, 0));
+    all.push_back(ROOF_VARIANT_OS(32, 8, 2, 2, 4));
+    all.push_back(ROOF_VARIANT_OS(32, 8, 2, 2, 8));
     all.push_back(CRC_VARIANT_W(32, 8, 2, 2, 1, 2, 33, 27));
     all.push_back(CRC_VARIANT_W(32, 8, 2, 2, 1, 2, 17, 13));
     all.push_back(CRC_VARIANT_W(32, 8, 2, 2, 1, 2, 9, 7));
@@ -303,6 +339,8 @@ int main(int argc, char **argv)
     for (int r = 0; r < rounds + 1; r++) { // round 0 = warm-up
         for (size_t vi = 0; vi <= V.size(); vi++) {
             Variant &v = vi < V.size() ? V[vi] : gs;
+            if (r == 0 && vi < V.size() && v.is_crc)
+                CK(hipMemset(d_out, 0xA5, nb * 4));
             CK(hipEventRecord(e0, 0));
             for (int it = 0; it < iters; it++) {
                 if (vi < V.size()) {
@@ -310,6 +348,7 @@ int main(int argc, char **argv)
                     const uint64_t want = (ng + kWaves - 1) / kWaves;
                     const uint32_t grid = (uint32_t)std::min<uint64_t>(want, (uint64_t)ncu * v.wg_per_cu);
                     v.launch(dim3(grid), 0, d, ng, bs, d_img[v.G], d_fold[v.G], v.is_crc ? d_out : d_sink);
+                    CK(hipGetLastError());
                 } else {
                     hipLaunchKernelGGL(roof_gridstride, dim3(ncu * 8), dim3(256), 0, 0, (const v4u *)d,
                                        (uint64_t)bs * nb / 16, d_sink);
