@@ -25,6 +25,7 @@
 
 namespace {
 #include "../priskv_amd/csrc/crc_device.inc"
+#include "crc_ranges2_explore.inc"
 } // namespace
 
 #define CK(x)                                                                                      \
@@ -43,6 +44,7 @@ struct Variant {
     const char *name;
     int wg_per_cu;
     LaunchFn launch;
+    bool g32; // two-stream kernel: G = 32 tables and fold columns
 };
 
 #define RV(CH, NB, AUX, WG)                                                                                    \
@@ -51,7 +53,14 @@ struct Variant {
                uint32_t lc, const uint32_t *img, const uint32_t *fold, const uint32_t *un, uint32_t *out) {       \
                 hipLaunchKernelGGL((crc_ranges_kernel<CH, NB, AUX>), g, dim3(kThreads), 0, 0, b, n, o, l, 0ull,   \
                                    stride, lc, img, fold, un, out);                                                \
-            }}
+            }, false}
+#define RV2(CH, NB, AUX, WG)                                                                                   \
+    Variant{"ext2 CH" #CH " NBUF" #NB " AUX" #AUX " wg/cu" #WG, WG,                                            \
+            [](dim3 g, const uint8_t *b, uint64_t n, const uint64_t *o, const uint32_t *l, uint64_t stride,       \
+               uint32_t lc, const uint32_t *img, const uint32_t *fold, const uint32_t *un, uint32_t *out) {       \
+                hipLaunchKernelGGL((crc_ranges2_kernel<CH, NB, AUX>), g, dim3(kThreads), 0, 0, b, n, o, l, 0ull,  \
+                                   stride, lc, img, fold, un, out);                                                \
+            }, true}
 
 struct Set {
     const char *name;
@@ -76,6 +85,14 @@ int main(int argc, char **argv)
     prv_lds_image(img.data(), 1008);
     prv_fold_columns(fold.data(), 64);
     prv_unshift_columns(un.data());
+    std::vector<uint32_t> img32(PRV_LDS_WORDS), fold32(2048);
+    prv_lds_image(img32.data(), 496);
+    prv_fold_columns(fold32.data(), 32);
+    uint32_t *d_img32, *d_fold32;
+    CK(hipMalloc(&d_img32, img32.size() * 4));
+    CK(hipMalloc(&d_fold32, fold32.size() * 4));
+    CK(hipMemcpy(d_img32, img32.data(), img32.size() * 4, hipMemcpyHostToDevice));
+    CK(hipMemcpy(d_fold32, fold32.data(), fold32.size() * 4, hipMemcpyHostToDevice));
     uint32_t *d_img, *d_fold, *d_un;
     CK(hipMalloc(&d_img, img.size() * 4));
     CK(hipMalloc(&d_fold, fold.size() * 4));
@@ -134,8 +151,8 @@ int main(int argc, char **argv)
         sets.push_back(w);
     }
 
-    std::vector<Variant> V = {RV(2, 2, 2, 2), RV(4, 2, 2, 2), RV(2, 3, 2, 2), RV(4, 3, 2, 2), RV(1, 4, 2, 2),
-                              RV(1, 3, 2, 2)};
+    std::vector<Variant> V = {RV(2, 2, 2, 2), RV2(2, 2, 2, 2), RV2(4, 2, 2, 2), RV2(2, 3, 2, 2), RV2(4, 2, 2, 1),
+                              RV2(8, 2, 2, 1)};
     uint64_t nmax = 0;
     for (auto &s : sets)
         nmax = std::max(nmax, s.n);
@@ -156,9 +173,12 @@ int main(int argc, char **argv)
                 const uint64_t want = (s.n + kWaves - 1) / kWaves;
                 const uint32_t grid = (uint32_t)std::min<uint64_t>(want, (uint64_t)ncu * V[vi].wg_per_cu);
                 CK(hipEventRecord(e0, 0));
+                if (r == 0)
+                    CK(hipMemset(d_out, 0xA5, s.n * 4));
                 for (int it = 0; it < iters; it++)
-                    V[vi].launch(dim3(grid), d, s.n, s.d_off, s.d_len, s.stride, s.len_const, d_img, d_fold, d_un,
-                                 d_out);
+                    V[vi].launch(dim3(grid), d, s.n, s.d_off, s.d_len, s.stride, s.len_const,
+                                 V[vi].g32 ? d_img32 : d_img, V[vi].g32 ? d_fold32 : d_fold, d_un, d_out);
+                CK(hipGetLastError());
                 CK(hipEventRecord(e1, 0));
                 CK(hipEventSynchronize(e1));
                 float t;
