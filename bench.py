@@ -251,7 +251,10 @@ def ctx_path(bs, region):
             g, ch = 64, (4 if r % 4 == 0 else (2 if r % 2 == 0 else 1))
         w = os.environ.get("PRISKV_CRC_XCD_WEIGHTS", "31:29")
         split = "" if w.replace(" ", "") in ("1:1",) else f",xcd-weighted {w}"
-        return f"crc_rows_kernel<G={g},CH={ch},NBUF=2,nt{',pipelined-fold' if pipe else ''}{split}>"
+        fold = ",pipelined-fold" if pipe else ""
+        if pipe:
+            fold += ",nibble-table-fold"
+        return f"crc_rows_kernel<G={g},CH={ch},NBUF=2,nt{fold}{split}>"
     return f"crc_{p}_kernel"
 
 

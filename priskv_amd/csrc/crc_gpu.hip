@@ -59,6 +59,7 @@ struct priskv_crc_ctx {
     uint32_t xcd_weights;      // rows-kernel split: (even << 16) | odd XCD weight, 0 = equal
     uint32_t *d_lds_image[3];  // 64 KiB each: set B gap for G = 64, 32, 16
     uint32_t *d_fold;          // kFoldSets x 2048 words, set j for G = 1 << j
+    uint32_t *d_nib[3];        // nibble fold tables (8 x 16 x G words) for G = 64, 32, 16
     uint32_t *d_sarwate;       // 256 words
     uint32_t *d_unshift;       // 16 x 32 words: columns of Z_-p, p = 0..15
     // host-streamed path (guarded by lock)
@@ -169,9 +170,9 @@ int launch_extents(const priskv_crc_ctx *ctx, const uint8_t *base, uint64_t n, c
 // (NBUF = 2) and cache policy (nt) are fixed.
 
 enum PlanId {
-    PLAN_G32_CH8_PIPE, // 4 KiB: one chunk == one 2-block group, fold pipelined
+    PLAN_G32_CH8_PIPE, // 4 KiB: one chunk == one 2-block group, fold pipelined, nibble-table fold
     PLAN_G32_CH8,      // 8 / 12 / 16 KiB
-    PLAN_G16_CH4_PIPE, // 1 KiB
+    PLAN_G16_CH4_PIPE, // 1 KiB (same two folds)
     PLAN_G16_CH4,      // other multiples of 1 KiB up to 16 KiB
     PLAN_G64_CH4,      // > 16 KiB
     PLAN_G64_CH2,
@@ -181,7 +182,8 @@ enum PlanId {
 struct Plan {
     int G, CH, opt, wg_per_cu;
 };
-constexpr Plan kPlans[NPLANS] = {{32, 8, 2, 1}, {32, 8, 0, 1}, {16, 4, 2, 2}, {16, 4, 0, 2},
+// opt = crc_rows_kernel OPT bits: 2 = pipelined fold, 32 = nibble-table fold
+constexpr Plan kPlans[NPLANS] = {{32, 8, 2 | 32, 1}, {32, 8, 0, 1}, {16, 4, 2 | 32, 2}, {16, 4, 0, 2},
                                  {64, 4, 0, 1}, {64, 2, 0, 1}, {64, 1, 0, 1}};
 
 int plan_for(uint32_t bs)
@@ -207,9 +209,9 @@ const void *plan_kernel()
 const void *plan_fn(int p)
 {
     switch (p) {
-    case PLAN_G32_CH8_PIPE: return plan_kernel<32, 8, 2>();
+    case PLAN_G32_CH8_PIPE: return plan_kernel<32, 8, 2 | 32>();
     case PLAN_G32_CH8: return plan_kernel<32, 8, 0>();
-    case PLAN_G16_CH4_PIPE: return plan_kernel<16, 4, 2>();
+    case PLAN_G16_CH4_PIPE: return plan_kernel<16, 4, 2 | 32>();
     case PLAN_G16_CH4: return plan_kernel<16, 4, 0>();
     case PLAN_G64_CH4: return plan_kernel<64, 4, 0>();
     case PLAN_G64_CH2: return plan_kernel<64, 2, 0>();
@@ -234,7 +236,7 @@ int launch_plan(const priskv_crc_ctx *ctx, int p, const uint8_t *base, uint64_t 
         const uint8_t *b = base + done * nb_per_group * bs;
         uint32_t *o = out + done * nb_per_group;
         const uint32_t *img = ctx->d_lds_image[gi];
-        const uint32_t *fold = ctx->d_fold + log2u(P.G) * 2048;
+        const uint32_t *fold = (P.opt & 32) ? ctx->d_nib[gi] : ctx->d_fold + log2u(P.G) * 2048;
         // weights move whole groups: only worth it with many groups per wave
         uint32_t xw = n >= 32ull * grid * kWaves ? ctx->xcd_weights : 0u;
         void *args[] = {(void *)&b, (void *)&n, (void *)&bs, (void *)&img, (void *)&fold, (void *)&o, (void *)&xw};
@@ -442,6 +444,10 @@ int priskv_crc_ctx_create(int device, priskv_crc_ctx **out)
         if ((rc = herr(hipMalloc((void **)&c->d_lds_image[gi], sizeof(uint32_t) * PRV_LDS_WORDS))) ||
             (rc = herr(hipMemcpy(c->d_lds_image[gi], h_img, sizeof(uint32_t) * PRV_LDS_WORDS, hipMemcpyHostToDevice))))
             goto fail;
+        prv_fold_nibbles(h_img, G); // 8 x 16 x G words fit in the image buffer
+        if ((rc = herr(hipMalloc((void **)&c->d_nib[gi], sizeof(uint32_t) * 8 * 16 * G))) ||
+            (rc = herr(hipMemcpy(c->d_nib[gi], h_img, sizeof(uint32_t) * 8 * 16 * G, hipMemcpyHostToDevice))))
+            goto fail;
     }
     if ((rc = rows_occupancy(c)))
         goto fail;
@@ -473,8 +479,10 @@ void priskv_crc_ctx_destroy(priskv_crc_ctx *c)
             (void)hipHostFree(c->h_out_stage[i]);
         }
     }
-    for (int gi = 0; gi < 3; gi++)
+    for (int gi = 0; gi < 3; gi++) {
         (void)hipFree(c->d_lds_image[gi]);
+        (void)hipFree(c->d_nib[gi]);
+    }
     (void)hipFree(c->d_fold);
     (void)hipFree(c->d_sarwate);
     (void)hipFree(c->d_unshift);

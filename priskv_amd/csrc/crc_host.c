@@ -185,6 +185,18 @@ void prv_fold_columns(uint32_t out[32 * 64], uint32_t group)
     }
 }
 
+void prv_fold_nibbles(uint32_t *out, uint32_t group)
+{
+    /* out[(16n + v)*G + c] = Z_(4 + 16(G-1-c))(v << 4n), G = group (16..64):
+     * the nibble tables of nib_fold (crc_device.inc) */
+    for (uint32_t c = 0; c < group; c++) {
+        const uint64_t dist = 4ull + 16ull * (group - 1 - c);
+        for (uint32_t n = 0; n < 8; n++)
+            for (uint32_t v = 0; v < 16; v++)
+                out[(16 * n + v) * group + c] = priskv_crc32_shift(v << (4 * n), dist);
+    }
+}
+
 /* one zero byte backwards: c' = T[c & 0xff] ^ (c >> 8) has top byte
  * T[c & 0xff] >> 24, and the top bytes of the 256 table entries are distinct,
  * so c & 0xff = b with T[b] >> 24 == c' >> 24 and c = ((c' ^ T[b]) << 8) | b */

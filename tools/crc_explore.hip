@@ -215,6 +215,16 @@ static uint32_t g_epoch = 0;
                                    (uint32_t)(((WE) << 16) | (WO)));                                       \
             }, {}}
 #define ROOF_VARIANT(G, CH, NB, AUX, WGPC) ROOF_VARIANT_W(G, CH, NB, AUX, WGPC, 0, 0)
+// nibble-table fold (OPT bit 5): the fold pointer is the nibble image
+static uint32_t *g_nib[65] = {};
+#define NIB_VARIANT_W(G, CH, NB, AUX, WGPC, OPT, WE, WO)                                                      \
+    Variant{"nib G" #G " CH" #CH " NBUF" #NB " AUX" #AUX " wg/cu" #WGPC " opt" #OPT " xw" #WE ":" #WO, true, G, \
+            CH, WGPC, OPT,                                                                                     \
+            [](dim3 g, hipStream_t s, const uint8_t *b, uint64_t n, uint32_t bs, const uint32_t *img,           \
+               const uint32_t *, uint32_t *o) {                                                                \
+                hipLaunchKernelGGL((crc_rows_kernel<G, CH, NB, AUX, (OPT) | 32>), g, dim3(kThreads), 0, s, b, n, bs, \
+                                   img, g_nib[G], o, (uint32_t)(((WE) << 16) | (WO)));                         \
+            }, {}}
 
 int main(int argc, char **argv)
 {
@@ -231,13 +241,16 @@ int main(int argc, char **argv)
     uint8_t *d;
     uint32_t *d_img[65] = {}, *d_fold[65] = {}, *d_out, *d_ref, *d_sink;
     for (int G = 16; G <= 64; G *= 2) {
-        std::vector<uint32_t> img(PRV_LDS_WORDS), fold(2048);
+        std::vector<uint32_t> img(PRV_LDS_WORDS), fold(2048), nib(8 * 16 * G);
         prv_lds_image(img.data(), 16u * G - 16u);
         prv_fold_columns(fold.data(), G);
+        prv_fold_nibbles(nib.data(), G);
         CK(hipMalloc(&d_img[G], img.size() * 4));
         CK(hipMalloc(&d_fold[G], fold.size() * 4));
+        CK(hipMalloc(&g_nib[G], nib.size() * 4));
         CK(hipMemcpy(d_img[G], img.data(), img.size() * 4, hipMemcpyHostToDevice));
         CK(hipMemcpy(d_fold[G], fold.data(), fold.size() * 4, hipMemcpyHostToDevice));
+        CK(hipMemcpy(g_nib[G], nib.data(), nib.size() * 4, hipMemcpyHostToDevice));
     }
     CK(hipMalloc(&d, (size_t)bs * nb));
     CK(hipMalloc(&d_out, nb * 4 + (size_t)ncu * 4 * kWaves * 8)); // + per-wave timestamps
@@ -252,7 +265,22 @@ int main(int argc, char **argv)
     CK(hipMemset(g_slots, 0, (size_t)ncu * 2 * kWaves * 128));
     std::vector<Variant> all;
     // first entry = product reference for the bit-exact cross-check and the sustained run
-    all.push_back(CRC_VARIANT(32, 8, 2, 2, 1, 2));
+    all.push_back(CRC_VARIANT_W(32, 8, 2, 2, 1, 2, 31, 29));
+    all.push_back(NIB_VARIANT_W(32, 8, 2, 2, 1, 2, 31, 29));
+    all.push_back(NIB_VARIANT_W(32, 8, 3, 2, 1, 2, 31, 29));
+    all.push_back(NIB_VARIANT_W(32, 8, 2, 2, 2, 2, 31, 29));
+    all.push_back(NIB_VARIANT_W(32, 8, 2, 2, 1, 6, 31, 29));
+    all.push_back(NIB_VARIANT_W(32, 8, 2, 2, 1, 0, 31, 29));
+    all.push_back(NIB_VARIANT_W(16, 16, 2, 2, 1, 2, 31, 29));
+    all.push_back(NIB_VARIANT_W(64, 4, 2, 2, 1, 0, 31, 29));
+    all.push_back(CRC_VARIANT_W(32, 8, 2, 2, 1, 0, 31, 29));
+    all.push_back(CRC_VARIANT_W(16, 4, 2, 2, 2, 2, 31, 29));
+    all.push_back(NIB_VARIANT_W(16, 4, 2, 2, 2, 2, 31, 29));
+    all.push_back(CRC_VARIANT_W(32, 8, 3, 2, 1, 2, 31, 29));
+    all.push_back(CRC_VARIANT_W(32, 8, 4, 2, 1, 2, 31, 29));
+    all.push_back(CRC_VARIANT_W(32, 8, 2, 2, 1, 6, 31, 29));
+    all.push_back(ROOF_VARIANT_W(32, 8, 3, 2, 1, 31, 29));
+    all.push_back(ROOF_VARIANT_W(32, 8, 2, 2, 1, 31, 29));
     all.push_back(PAIR_VARIANT(32, 8, 2, 2, 1, 2));
     all.push_back(PAIR_VARIANT(32, 8, 2, 2, 1, 10));
     all.push_back(PAIR_VARIANT(32, 8, 2, 2, 1, 66));
