@@ -61,7 +61,7 @@ struct priskv_crc_ctx {
     uint32_t *d_fold;          // kFoldSets x 2048 words, set j for G = 1 << j
     uint32_t *d_nib[3];        // nibble fold tables (8 x 16 x G words) for G = 64, 32, 16
     uint32_t *d_sarwate;       // 256 words
-    uint32_t *d_unshift;       // 16 x 32 words: columns of Z_-p, p = 0..15
+    uint32_t *d_rowshift;      // 16 x 4 x 32 words: columns of Z_-p o Z_(256(3-k)) (extents fold)
     // host-streamed path (guarded by lock)
     pthread_mutex_t lock;
     int stream_ready;
@@ -148,6 +148,7 @@ int launch_generic(const priskv_crc_ctx *ctx, const uint8_t *base, uint64_t n, u
 constexpr int kNbuf = 2;  // register pipeline depth (chunks)
 constexpr int kAux = 2;   // cache policy of the streaming loads: nt
 constexpr int kExtRows = 2; // rows per chunk of the extents kernel (tools/ranges_explore)
+constexpr int kExtOpt = 3;  // extents kernel: nibble fold + row apply (bit 0), masks only where needed (bit 1)
 
 // extents through the row machinery (any base alignment, any lengths)
 int launch_extents(const priskv_crc_ctx *ctx, const uint8_t *base, uint64_t n, const uint64_t *offs,
@@ -158,8 +159,8 @@ int launch_extents(const priskv_crc_ctx *ctx, const uint8_t *base, uint64_t n, c
     const uint64_t want = (n + kWaves - 1) / kWaves;
     const uint64_t cap = (uint64_t)ctx->num_cus * 2;
     const uint32_t grid = (uint32_t)(want < cap ? want : cap);
-    hipLaunchKernelGGL((crc_ranges_kernel<kExtRows, kNbuf, kAux>), dim3(grid), dim3(kThreads), 0, s, abase, n, offs,
-                       lens, shift, stride, len_const, ctx->d_lds_image[0], ctx->d_fold + 6 * 2048, ctx->d_unshift,
+    hipLaunchKernelGGL((crc_ranges_kernel<kExtRows, kNbuf, kAux, kExtOpt>), dim3(grid), dim3(kThreads), 0, s, abase,
+                       n, offs, lens, shift, stride, len_const, ctx->d_lds_image[0], ctx->d_nib[2], ctx->d_rowshift,
                        out);
     return herr(hipGetLastError());
 }
@@ -417,7 +418,7 @@ int priskv_crc_ctx_create(int device, priskv_crc_ctx **out)
     uint32_t *h_img = (uint32_t *)malloc(sizeof(uint32_t) * PRV_LDS_WORDS);
     uint32_t *h_fold = (uint32_t *)malloc(sizeof(uint32_t) * 2048 * kFoldSets);
     uint32_t h_sar[256];
-    uint32_t h_unshift[16 * 32];
+    static_assert(16 * 4 * 32 <= PRV_LDS_WORDS, "rowshift image fits the staging buffer");
     if (!h_img || !h_fold) {
         rc = -ENOMEM;
         goto fail;
@@ -429,14 +430,15 @@ int priskv_crc_ctx_create(int device, priskv_crc_ctx **out)
     for (int j = 0; j < kFoldSets; j++)
         prv_fold_columns(h_fold + j * 2048, 1u << j);
     prv_sarwate_table(h_sar);
-    prv_unshift_columns(h_unshift);
     if ((rc = herr(hipMalloc((void **)&c->d_fold, sizeof(uint32_t) * 2048 * kFoldSets))) ||
         (rc = herr(hipMalloc((void **)&c->d_sarwate, sizeof(h_sar)))) ||
-        (rc = herr(hipMalloc((void **)&c->d_unshift, sizeof(h_unshift)))))
+        (rc = herr(hipMalloc((void **)&c->d_rowshift, sizeof(uint32_t) * 16 * 4 * 32))))
         goto fail;
     if ((rc = herr(hipMemcpy(c->d_fold, h_fold, sizeof(uint32_t) * 2048 * kFoldSets, hipMemcpyHostToDevice))) ||
-        (rc = herr(hipMemcpy(c->d_sarwate, h_sar, sizeof(h_sar), hipMemcpyHostToDevice))) ||
-        (rc = herr(hipMemcpy(c->d_unshift, h_unshift, sizeof(h_unshift), hipMemcpyHostToDevice))))
+        (rc = herr(hipMemcpy(c->d_sarwate, h_sar, sizeof(h_sar), hipMemcpyHostToDevice))))
+        goto fail;
+    prv_rowshift_columns(h_img);
+    if ((rc = herr(hipMemcpy(c->d_rowshift, h_img, sizeof(uint32_t) * 16 * 4 * 32, hipMemcpyHostToDevice))))
         goto fail;
     for (int gi = 0; gi < 3; gi++) {
         const uint32_t G = 64u >> gi; // 64, 32, 16
@@ -485,7 +487,7 @@ void priskv_crc_ctx_destroy(priskv_crc_ctx *c)
     }
     (void)hipFree(c->d_fold);
     (void)hipFree(c->d_sarwate);
-    (void)hipFree(c->d_unshift);
+    (void)hipFree(c->d_rowshift);
     (void)hipFree(c->d_scrub);
     if (c->aux)
         (void)hipStreamDestroy(c->aux);

@@ -221,6 +221,23 @@ void prv_unshift_columns(uint32_t out[16 * 32])
     }
 }
 
+void prv_rowshift_columns(uint32_t out[16 * 4 * 32])
+{
+    /* out[(4p + k)*32 + j] = Z_-p(Z_(256(3-k))(1 << j)): row k's total of the
+     * extents kernel's nibble fold, shifted to the extent end and back over p
+     * pad bytes */
+    uint32_t un[16 * 32];
+    prv_unshift_columns(un);
+    for (int p = 0; p < 16; p++)
+        for (int k = 0; k < 4; k++)
+            for (int j = 0; j < 32; j++) {
+                uint32_t cols[32];
+                for (int i = 0; i < 32; i++)
+                    cols[i] = un[p * 32 + i];
+                out[(4 * p + k) * 32 + j] = mat_apply(cols, priskv_crc32_shift(1u << j, 256u * (3 - k)));
+            }
+}
+
 void prv_sarwate_table(uint32_t out[256])
 {
     pthread_once(&g_once, host_init);

@@ -34,6 +34,8 @@ PRV_HIDDEN uint32_t prv_crc32_clmul(uint32_t crc, const uint8_t *p, uint64_t len
 PRV_HIDDEN uint32_t prv_crc32_vclmul(uint32_t crc, const uint8_t *p, uint64_t len);
 /* out[p*32 + i] = column i of Z_-p (p = 0..15): undoes p trailing zero bytes */
 PRV_HIDDEN void prv_unshift_columns(uint32_t out[16 * 32]);
+/* out[(4p + k)*32 + j] = column j of Z_-p o Z_(256(3-k)) (extents nibble fold) */
+PRV_HIDDEN void prv_rowshift_columns(uint32_t out[16 * 4 * 32]);
 
 #if defined(__cplusplus)
 }

@@ -1,0 +1,9 @@
+# extents kernel opt3 adopted: full gpu tests, every-path sweep, bench
+set -e
+R=$GRAFT_REPO_ROOT
+O=$R/gpurun_out/r1zs
+mkdir -p $O
+timeout -k 10 600 python -u -m pytest tests -x -v -m gpu --timeout 300 --timeout-method thread > $O/pytest.log 2>&1
+timeout -k 10 500 python tools/bench_paths.py > $O/paths.jsonl 2> $O/paths.err
+timeout -k 10 300 python bench.py > $O/bench.log 2>&1
+echo ALLDONE

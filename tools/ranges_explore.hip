@@ -62,6 +62,17 @@ struct Variant {
                                    stride, lc, img, fold, un, out);                                                \
             }, true}
 
+// OPT bit 0 (nibble fold) takes its two images from these globals
+static uint32_t *g_nib16 = nullptr, *g_rowshift = nullptr;
+#define RVO(CH, NB, AUX, WG, OPT)                                                                              \
+    Variant{"ext CH" #CH " NBUF" #NB " AUX" #AUX " wg/cu" #WG " opt" #OPT, WG,                                 \
+            [](dim3 g, const uint8_t *b, uint64_t n, const uint64_t *o, const uint32_t *l, uint64_t stride,       \
+               uint32_t lc, const uint32_t *img, const uint32_t *fold, const uint32_t *un, uint32_t *out) {       \
+                hipLaunchKernelGGL((crc_ranges_kernel<CH, NB, AUX, OPT>), g, dim3(kThreads), 0, 0, b, n, o, l,     \
+                                   0ull, stride, lc, img, ((OPT) & 1) ? g_nib16 : fold,                           \
+                                   ((OPT) & 1) ? g_rowshift : un, out);                                           \
+            }, false}
+
 struct Set {
     const char *name;
     uint64_t n, stride;
@@ -100,6 +111,15 @@ int main(int argc, char **argv)
     CK(hipMemcpy(d_img, img.data(), img.size() * 4, hipMemcpyHostToDevice));
     CK(hipMemcpy(d_fold, fold.data(), fold.size() * 4, hipMemcpyHostToDevice));
     CK(hipMemcpy(d_un, un.data(), un.size() * 4, hipMemcpyHostToDevice));
+    {
+        std::vector<uint32_t> nib(8 * 16 * 16), rs(16 * 4 * 32);
+        prv_fold_nibbles(nib.data(), 16);
+        prv_rowshift_columns(rs.data());
+        CK(hipMalloc(&g_nib16, nib.size() * 4));
+        CK(hipMalloc(&g_rowshift, rs.size() * 4));
+        CK(hipMemcpy(g_nib16, nib.data(), nib.size() * 4, hipMemcpyHostToDevice));
+        CK(hipMemcpy(g_rowshift, rs.data(), rs.size() * 4, hipMemcpyHostToDevice));
+    }
 
     // PrisKV-shaped extents (as tools/bench_paths.py extents())
     const uint64_t n = 1 << 19, bs = 4096;
@@ -151,8 +171,8 @@ int main(int argc, char **argv)
         sets.push_back(w);
     }
 
-    std::vector<Variant> V = {RV(2, 2, 2, 2), RV2(2, 2, 2, 2), RV2(4, 2, 2, 2), RV2(2, 3, 2, 2), RV2(4, 2, 2, 1),
-                              RV2(8, 2, 2, 1)};
+    std::vector<Variant> V = {RV(2, 2, 2, 2),         RVO(2, 2, 2, 2, 1), RVO(2, 2, 2, 2, 2), RVO(2, 2, 2, 2, 3),
+                              RVO(1, 4, 2, 2, 3),     RVO(2, 3, 2, 2, 3), RVO(4, 2, 2, 2, 3)};
     uint64_t nmax = 0;
     for (auto &s : sets)
         nmax = std::max(nmax, s.n);
