@@ -242,9 +242,9 @@ def ctx_path(bs, region):
     p = blocks_path(region.data_ptr(), 1, bs)
     if p == "rows":
         pipe = bs in (1024, 4096)
-        if bs <= 16384 and bs % 4096 == 0:
+        if bs == 4096:
             g, ch = 32, 8
-        elif bs <= 16384:
+        elif bs <= 16384 and bs % 4096:
             g, ch = 16, 4
         else:
             r = bs // 1024
@@ -252,7 +252,7 @@ def ctx_path(bs, region):
         w = os.environ.get("PRISKV_CRC_XCD_WEIGHTS", "31:29")
         split = "" if w.replace(" ", "") in ("1:1",) else f",xcd-weighted {w}"
         fold = ",pipelined-fold" if pipe else ""
-        if pipe:
+        if bs in (1024, 4096, 8192):
             fold += ",nibble-table-fold"
         return f"crc_rows_kernel<G={g},CH={ch},NBUF=2,nt{fold}{split}>"
     return f"crc_{p}_kernel"

@@ -59,7 +59,8 @@ struct priskv_crc_ctx {
     uint32_t xcd_weights;      // rows-kernel split: (even << 16) | odd XCD weight, 0 = equal
     uint32_t *d_lds_image[3];  // 64 KiB each: set B gap for G = 64, 32, 16
     uint32_t *d_fold;          // kFoldSets x 2048 words, set j for G = 1 << j
-    uint32_t *d_nib[3];        // nibble fold tables (8 x 16 x G words) for G = 64, 32, 16
+    uint32_t *d_nibrep[7];     // nibble fold tables for G = 1 << j (j >= 1), 8 x 16 x max(G, 32) words
+    uint32_t *d_nib16;         // the extents kernel's: G = 16, width 16 (8 KiB)
     uint32_t *d_sarwate;       // 256 words
     uint32_t *d_rowshift;      // 16 x 4 x 32 words: columns of Z_-p o Z_(256(3-k)) (extents fold)
     // host-streamed path (guarded by lock)
@@ -160,7 +161,7 @@ int launch_extents(const priskv_crc_ctx *ctx, const uint8_t *base, uint64_t n, c
     const uint64_t cap = (uint64_t)ctx->num_cus * 2;
     const uint32_t grid = (uint32_t)(want < cap ? want : cap);
     hipLaunchKernelGGL((crc_ranges_kernel<kExtRows, kNbuf, kAux, kExtOpt>), dim3(grid), dim3(kThreads), 0, s, abase,
-                       n, offs, lens, shift, stride, len_const, ctx->d_lds_image[0], ctx->d_nib[2], ctx->d_rowshift,
+                       n, offs, lens, shift, stride, len_const, ctx->d_lds_image[0], ctx->d_nib16, ctx->d_rowshift,
                        out);
     return herr(hipGetLastError());
 }
@@ -172,10 +173,10 @@ int launch_extents(const priskv_crc_ctx *ctx, const uint8_t *base, uint64_t n, c
 
 enum PlanId {
     PLAN_G32_CH8_PIPE, // 4 KiB: one chunk == one 2-block group, fold pipelined, nibble-table fold
-    PLAN_G32_CH8,      // 8 / 12 / 16 KiB
+    PLAN_G64_CH4_NIB,  // 8 KiB: G64 with the nibble fold (every 2 chunks)
     PLAN_G16_CH4_PIPE, // 1 KiB (same two folds)
     PLAN_G16_CH4,      // other multiples of 1 KiB up to 16 KiB
-    PLAN_G64_CH4,      // > 16 KiB
+    PLAN_G64_CH4,      // 12 KiB and up (multiples of 4 KiB)
     PLAN_G64_CH2,
     PLAN_G64_CH1,
     NPLANS
@@ -184,18 +185,18 @@ struct Plan {
     int G, CH, opt, wg_per_cu;
 };
 // opt = crc_rows_kernel OPT bits: 2 = pipelined fold, 32 = nibble-table fold
-constexpr Plan kPlans[NPLANS] = {{32, 8, 2 | 32, 1}, {32, 8, 0, 1}, {16, 4, 2 | 32, 2}, {16, 4, 0, 2},
+constexpr Plan kPlans[NPLANS] = {{32, 8, 2 | 32, 1}, {64, 4, 32, 1}, {16, 4, 2 | 32, 2}, {16, 4, 0, 2},
                                  {64, 4, 0, 1}, {64, 2, 0, 1}, {64, 1, 0, 1}};
 
 int plan_for(uint32_t bs)
 {
     if (bs == 4096)
         return PLAN_G32_CH8_PIPE;
-    if (bs <= (16u << 10) && bs % 4096 == 0)
-        return PLAN_G32_CH8;
+    if (bs == 8192)
+        return PLAN_G64_CH4_NIB;
     if (bs == 1024)
         return PLAN_G16_CH4_PIPE;
-    if (bs <= (16u << 10))
+    if (bs <= (16u << 10) && bs % 4096 != 0)
         return PLAN_G16_CH4;
     const uint32_t R = bs / PRV_ROW_BYTES;
     return R % 4 == 0 ? PLAN_G64_CH4 : (R % 2 == 0 ? PLAN_G64_CH2 : PLAN_G64_CH1);
@@ -211,7 +212,7 @@ const void *plan_fn(int p)
 {
     switch (p) {
     case PLAN_G32_CH8_PIPE: return plan_kernel<32, 8, 2 | 32>();
-    case PLAN_G32_CH8: return plan_kernel<32, 8, 0>();
+    case PLAN_G64_CH4_NIB: return plan_kernel<64, 4, 32>();
     case PLAN_G16_CH4_PIPE: return plan_kernel<16, 4, 2 | 32>();
     case PLAN_G16_CH4: return plan_kernel<16, 4, 0>();
     case PLAN_G64_CH4: return plan_kernel<64, 4, 0>();
@@ -237,7 +238,7 @@ int launch_plan(const priskv_crc_ctx *ctx, int p, const uint8_t *base, uint64_t 
         const uint8_t *b = base + done * nb_per_group * bs;
         uint32_t *o = out + done * nb_per_group;
         const uint32_t *img = ctx->d_lds_image[gi];
-        const uint32_t *fold = (P.opt & 32) ? ctx->d_nib[gi] : ctx->d_fold + log2u(P.G) * 2048;
+        const uint32_t *fold = (P.opt & 32) ? ctx->d_nibrep[log2u(P.G)] : ctx->d_fold + log2u(P.G) * 2048;
         // weights move whole groups: only worth it with many groups per wave
         uint32_t xw = n >= 32ull * grid * kWaves ? ctx->xcd_weights : 0u;
         void *args[] = {(void *)&b, (void *)&n, (void *)&bs, (void *)&img, (void *)&fold, (void *)&o, (void *)&xw};
@@ -329,15 +330,16 @@ int launch_blocks(const priskv_crc_ctx *ctx, const uint8_t *base, uint64_t nbloc
         if (nrows) {
             uint64_t want = (nrows + 4 * kWaves - 1) / (4 * kWaves);
             uint32_t grid = (uint32_t)(want < (uint64_t)ctx->max_wgs ? want : (uint64_t)ctx->max_wgs);
-            const uint32_t *fold = ctx->d_fold + gl * 2048;
+            // G >= 2: nibble-table fold (replicated 32-wide tables)
+            const uint32_t *fold = gl ? ctx->d_nibrep[gl] : ctx->d_fold;
             const uint32_t *img = ctx->d_lds_image[0];
             switch (gl) {
-            case 0: hipLaunchKernelGGL(crc_small_kernel<1>, dim3(grid), dim3(kThreads), 0, s, base, nrows, img, fold, out); break;
-            case 1: hipLaunchKernelGGL(crc_small_kernel<2>, dim3(grid), dim3(kThreads), 0, s, base, nrows, img, fold, out); break;
-            case 2: hipLaunchKernelGGL(crc_small_kernel<4>, dim3(grid), dim3(kThreads), 0, s, base, nrows, img, fold, out); break;
-            case 3: hipLaunchKernelGGL(crc_small_kernel<8>, dim3(grid), dim3(kThreads), 0, s, base, nrows, img, fold, out); break;
-            case 4: hipLaunchKernelGGL(crc_small_kernel<16>, dim3(grid), dim3(kThreads), 0, s, base, nrows, img, fold, out); break;
-            default: hipLaunchKernelGGL(crc_small_kernel<32>, dim3(grid), dim3(kThreads), 0, s, base, nrows, img, fold, out); break;
+            case 0: hipLaunchKernelGGL((crc_small_kernel<1, 0>), dim3(grid), dim3(kThreads), 0, s, base, nrows, img, fold, out); break;
+            case 1: hipLaunchKernelGGL((crc_small_kernel<2, 1>), dim3(grid), dim3(kThreads), 0, s, base, nrows, img, fold, out); break;
+            case 2: hipLaunchKernelGGL((crc_small_kernel<4, 1>), dim3(grid), dim3(kThreads), 0, s, base, nrows, img, fold, out); break;
+            case 3: hipLaunchKernelGGL((crc_small_kernel<8, 1>), dim3(grid), dim3(kThreads), 0, s, base, nrows, img, fold, out); break;
+            case 4: hipLaunchKernelGGL((crc_small_kernel<16, 1>), dim3(grid), dim3(kThreads), 0, s, base, nrows, img, fold, out); break;
+            default: hipLaunchKernelGGL((crc_small_kernel<32, 1>), dim3(grid), dim3(kThreads), 0, s, base, nrows, img, fold, out); break;
             }
             if (int rc = herr(hipGetLastError()))
                 return rc;
@@ -446,11 +448,18 @@ int priskv_crc_ctx_create(int device, priskv_crc_ctx **out)
         if ((rc = herr(hipMalloc((void **)&c->d_lds_image[gi], sizeof(uint32_t) * PRV_LDS_WORDS))) ||
             (rc = herr(hipMemcpy(c->d_lds_image[gi], h_img, sizeof(uint32_t) * PRV_LDS_WORDS, hipMemcpyHostToDevice))))
             goto fail;
-        prv_fold_nibbles(h_img, G); // 8 x 16 x G words fit in the image buffer
-        if ((rc = herr(hipMalloc((void **)&c->d_nib[gi], sizeof(uint32_t) * 8 * 16 * G))) ||
-            (rc = herr(hipMemcpy(c->d_nib[gi], h_img, sizeof(uint32_t) * 8 * 16 * G, hipMemcpyHostToDevice))))
+    }
+    for (int j = 1; j < kFoldSets; j++) {
+        const uint32_t G = 1u << j, W = G > 32 ? G : 32;
+        prv_fold_nibbles(h_img, G, W); // 8 x 16 x W words fit in the image buffer
+        if ((rc = herr(hipMalloc((void **)&c->d_nibrep[j], sizeof(uint32_t) * 8 * 16 * W))) ||
+            (rc = herr(hipMemcpy(c->d_nibrep[j], h_img, sizeof(uint32_t) * 8 * 16 * W, hipMemcpyHostToDevice))))
             goto fail;
     }
+    prv_fold_nibbles(h_img, 16, 16);
+    if ((rc = herr(hipMalloc((void **)&c->d_nib16, sizeof(uint32_t) * 8 * 16 * 16))) ||
+        (rc = herr(hipMemcpy(c->d_nib16, h_img, sizeof(uint32_t) * 8 * 16 * 16, hipMemcpyHostToDevice))))
+        goto fail;
     if ((rc = rows_occupancy(c)))
         goto fail;
     if ((rc = herr(hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking))))
@@ -481,10 +490,11 @@ void priskv_crc_ctx_destroy(priskv_crc_ctx *c)
             (void)hipHostFree(c->h_out_stage[i]);
         }
     }
-    for (int gi = 0; gi < 3; gi++) {
+    for (int gi = 0; gi < 3; gi++)
         (void)hipFree(c->d_lds_image[gi]);
-        (void)hipFree(c->d_nib[gi]);
-    }
+    for (int j = 0; j < kFoldSets; j++)
+        (void)hipFree(c->d_nibrep[j]);
+    (void)hipFree(c->d_nib16);
     (void)hipFree(c->d_fold);
     (void)hipFree(c->d_sarwate);
     (void)hipFree(c->d_rowshift);

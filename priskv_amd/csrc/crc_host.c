@@ -185,15 +185,16 @@ void prv_fold_columns(uint32_t out[32 * 64], uint32_t group)
     }
 }
 
-void prv_fold_nibbles(uint32_t *out, uint32_t group)
+void prv_fold_nibbles(uint32_t *out, uint32_t group, uint32_t width)
 {
-    /* out[(16n + v)*G + c] = Z_(4 + 16(G-1-c))(v << 4n), G = group (16..64):
-     * the nibble tables of nib_fold (crc_device.inc) */
-    for (uint32_t c = 0; c < group; c++) {
-        const uint64_t dist = 4ull + 16ull * (group - 1 - c);
+    /* out[(16n + v)*width + s] = Z_(4 + 16(G-1-s%G))(v << 4n), G = group
+     * (2..64), width a multiple of G: the nibble tables of nib_fold
+     * (crc_device.inc), one slot per lane of a ds_read half */
+    for (uint32_t sl = 0; sl < width; sl++) {
+        const uint64_t dist = 4ull + 16ull * (group - 1 - sl % group);
         for (uint32_t n = 0; n < 8; n++)
             for (uint32_t v = 0; v < 16; v++)
-                out[(16 * n + v) * group + c] = priskv_crc32_shift(v << (4 * n), dist);
+                out[(16 * n + v) * width + sl] = priskv_crc32_shift(v << (4 * n), dist);
     }
 }
 

@@ -22,8 +22,8 @@ extern "C"
 
 PRV_HIDDEN void prv_lds_image(uint32_t out[PRV_LDS_WORDS], uint32_t gap_bytes);
 PRV_HIDDEN void prv_fold_columns(uint32_t out[32 * 64], uint32_t group);
-/* nibble fold tables, 8*16*group words (crc_device.inc nib_fold) */
-PRV_HIDDEN void prv_fold_nibbles(uint32_t *out, uint32_t group);
+/* nibble fold tables, 8*16*width words (crc_device.inc nib_fold) */
+PRV_HIDDEN void prv_fold_nibbles(uint32_t *out, uint32_t group, uint32_t width);
 PRV_HIDDEN void prv_shift_columns(uint32_t out[32], uint64_t nbytes);
 PRV_HIDDEN void prv_sarwate_table(uint32_t out[256]);
 /* host CRC register update (init = crc, no xor): tables; clmul folding for

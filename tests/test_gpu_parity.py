@@ -77,8 +77,9 @@ def test_golden_ranges_on_gpu(torch_cuda, ctx, golden):
 
 # block sizes covering every dispatch path and rows-kernel plan
 # (priskv_amd/csrc/crc_gpu.hip plan_for):
-#   G32/CH8 (4K, 8K, 12K, 16K), G16/CH4 (1K, 2K, 3K, 5K, 6K),
-#   G64/CH4 (20K, 64K, 1M), G64/CH2 (18K), G64/CH1 (17K, 33K),
+#   G32/CH8 pipelined nibble fold (4K), G16/CH4 pipelined nibble fold (1K),
+#   G64/CH4 nibble fold (8K), G16/CH4 (2K, 3K, 5K, 6K),
+#   G64/CH4 (12K, 16K, 20K, 64K, 1M), G64/CH2 (18K), G64/CH1 (17K, 33K),
 #   sub-KiB (16..512), extents (>= 1 KiB not a multiple of 1 KiB), generic (smaller odd sizes)
 BLOCK_SIZES = [1024, 2048, 3072, 4096, 5120, 6144, 8192, 12288, 16384, 17408, 18432, 20480, 33792,
                65536, 1 << 20, 16, 32, 64, 128, 256, 512, 1, 3, 100, 1000, 4097, 4100, 48, 1025, 1040,

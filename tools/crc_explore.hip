@@ -226,6 +226,81 @@ static uint32_t *g_nib[65] = {};
                                    img, g_nib[G], o, (uint32_t)(((WE) << 16) | (WO)));                         \
             }, {}}
 
+// sub-KiB blocks: crc_small_kernel<G> with the bit-matrix fold (OPT 0) against
+// the nibble fold (OPT 1), interleaved, bit-identity checked
+template <int G>
+void small_pair(const uint8_t *d, uint64_t nrows, const uint32_t *img, const uint32_t *fold, const uint32_t *nib,
+                uint32_t *o, uint32_t grid, int opt)
+{
+    if (opt)
+        hipLaunchKernelGGL((crc_small_kernel<G, 1>), dim3(grid), dim3(kThreads), 0, 0, d, nrows, img, nib, o);
+    else
+        hipLaunchKernelGGL((crc_small_kernel<G, 0>), dim3(grid), dim3(kThreads), 0, 0, d, nrows, img, fold, o);
+}
+
+int small_ab(uint32_t bs, uint64_t nb, int rounds, int ncu)
+{
+    const int G = (int)bs / 16, W = std::max(G, 32);
+    std::vector<uint32_t> img(PRV_LDS_WORDS), fold(2048), nib(8 * 16 * W);
+    prv_lds_image(img.data(), 1008);
+    prv_fold_columns(fold.data(), G);
+    prv_fold_nibbles(nib.data(), G, W);
+    uint8_t *d;
+    uint32_t *d_img, *d_fold, *d_nib, *o0, *o1;
+    CK(hipMalloc(&d, (size_t)bs * nb));
+    CK(hipMalloc(&d_img, img.size() * 4));
+    CK(hipMalloc(&d_fold, fold.size() * 4));
+    CK(hipMalloc(&d_nib, nib.size() * 4));
+    CK(hipMalloc(&o0, nb * 4));
+    CK(hipMalloc(&o1, nb * 4));
+    CK(hipMemcpy(d_img, img.data(), img.size() * 4, hipMemcpyHostToDevice));
+    CK(hipMemcpy(d_fold, fold.data(), fold.size() * 4, hipMemcpyHostToDevice));
+    CK(hipMemcpy(d_nib, nib.data(), nib.size() * 4, hipMemcpyHostToDevice));
+    hipLaunchKernelGGL(fill_splitmix_kernel, dim3(ncu * 16), dim3(256), 0, 0, d, (uint64_t)bs * nb, 0x5EED5EEDull,
+                       0ull);
+    const uint64_t nrows = nb / (1024 / bs);
+    const uint64_t want = (nrows + 4 * kWaves - 1) / (4 * kWaves);
+    const uint32_t grid = (uint32_t)std::min<uint64_t>(want, (uint64_t)ncu * 2);
+    auto run = [&](int opt) {
+        uint32_t *o = opt ? o1 : o0;
+        switch (G) {
+        case 2: small_pair<2>(d, nrows, d_img, d_fold, d_nib, o, grid, opt); break;
+        case 4: small_pair<4>(d, nrows, d_img, d_fold, d_nib, o, grid, opt); break;
+        case 8: small_pair<8>(d, nrows, d_img, d_fold, d_nib, o, grid, opt); break;
+        case 16: small_pair<16>(d, nrows, d_img, d_fold, d_nib, o, grid, opt); break;
+        default: small_pair<32>(d, nrows, d_img, d_fold, d_nib, o, grid, opt); break;
+        }
+    };
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    std::vector<float> ms[2];
+    for (int r = 0; r < rounds + 1; r++)
+        for (int opt = 0; opt < 2; opt++) {
+            CK(hipEventRecord(e0, 0));
+            for (int it = 0; it < 5; it++)
+                run(opt);
+            CK(hipEventRecord(e1, 0));
+            CK(hipEventSynchronize(e1));
+            float t;
+            CK(hipEventElapsedTime(&t, e0, e1));
+            if (r)
+                ms[opt].push_back(t / 5);
+        }
+    std::vector<uint32_t> a(nb), b(nb);
+    CK(hipMemcpy(a.data(), o0, nb * 4, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(b.data(), o1, nb * 4, hipMemcpyDeviceToHost));
+    const bool same = !memcmp(a.data(), b.data(), nb * 4);
+    for (int opt = 0; opt < 2; opt++) {
+        std::sort(ms[opt].begin(), ms[opt].end());
+        const double med = ms[opt][ms[opt].size() / 2];
+        printf("small G%d %-12s median %8.4f ms  %7.1f GB/s (best %7.1f)\n", G, opt ? "nibble-fold" : "bit-matrix", med,
+               (double)bs * nb / med / 1e6, (double)bs * nb / ms[opt][0] / 1e6);
+    }
+    printf("small variants bit-identical: %s\n", same ? "yes" : "NO");
+    return same ? 0 : 1;
+}
+
 int main(int argc, char **argv)
 {
     const uint32_t bs = argc > 1 ? (uint32_t)atoi(argv[1]) : 4096;
@@ -241,10 +316,10 @@ int main(int argc, char **argv)
     uint8_t *d;
     uint32_t *d_img[65] = {}, *d_fold[65] = {}, *d_out, *d_ref, *d_sink;
     for (int G = 16; G <= 64; G *= 2) {
-        std::vector<uint32_t> img(PRV_LDS_WORDS), fold(2048), nib(8 * 16 * G);
+        std::vector<uint32_t> img(PRV_LDS_WORDS), fold(2048), nib(8 * 16 * std::max(G, 32));
         prv_lds_image(img.data(), 16u * G - 16u);
         prv_fold_columns(fold.data(), G);
-        prv_fold_nibbles(nib.data(), G);
+        prv_fold_nibbles(nib.data(), G, std::max(G, 32));
         CK(hipMalloc(&d_img[G], img.size() * 4));
         CK(hipMalloc(&d_fold[G], fold.size() * 4));
         CK(hipMalloc(&g_nib[G], nib.size() * 4));
@@ -252,6 +327,8 @@ int main(int argc, char **argv)
         CK(hipMemcpy(d_fold[G], fold.data(), fold.size() * 4, hipMemcpyHostToDevice));
         CK(hipMemcpy(g_nib[G], nib.data(), nib.size() * 4, hipMemcpyHostToDevice));
     }
+    if (bs <= 512)
+        return small_ab(bs, nb, rounds, ncu);
     CK(hipMalloc(&d, (size_t)bs * nb));
     CK(hipMalloc(&d_out, nb * 4 + (size_t)ncu * 4 * kWaves * 8)); // + per-wave timestamps
     CK(hipMalloc(&d_ref, nb * 4));
@@ -273,6 +350,10 @@ int main(int argc, char **argv)
     all.push_back(NIB_VARIANT_W(32, 8, 2, 2, 1, 0, 31, 29));
     all.push_back(NIB_VARIANT_W(16, 16, 2, 2, 1, 2, 31, 29));
     all.push_back(NIB_VARIANT_W(64, 4, 2, 2, 1, 0, 31, 29));
+    all.push_back(NIB_VARIANT_W(64, 8, 2, 2, 1, 2, 31, 29));
+    all.push_back(NIB_VARIANT_W(64, 16, 2, 2, 1, 2, 31, 29));
+    all.push_back(NIB_VARIANT_W(32, 16, 2, 2, 1, 2, 31, 29));
+    all.push_back(CRC_VARIANT_W(64, 8, 2, 2, 1, 2, 31, 29));
     all.push_back(CRC_VARIANT_W(32, 8, 2, 2, 1, 0, 31, 29));
     all.push_back(CRC_VARIANT_W(16, 4, 2, 2, 2, 2, 31, 29));
     all.push_back(NIB_VARIANT_W(16, 4, 2, 2, 2, 2, 31, 29));

@@ -113,7 +113,7 @@ int main(int argc, char **argv)
     CK(hipMemcpy(d_un, un.data(), un.size() * 4, hipMemcpyHostToDevice));
     {
         std::vector<uint32_t> nib(8 * 16 * 16), rs(16 * 4 * 32);
-        prv_fold_nibbles(nib.data(), 16);
+        prv_fold_nibbles(nib.data(), 16, 16);
         prv_rowshift_columns(rs.data());
         CK(hipMalloc(&g_nib16, nib.size() * 4));
         CK(hipMalloc(&g_rowshift, rs.size() * 4));
