@@ -57,11 +57,13 @@ struct priskv_crc_ctx {
     int max_wgs;               // resident workgroups of the sub-KiB kernel (2 per CU)
     int plan_wgs_per_cu[8];    // resident workgroups per CU of each rows-kernel plan
     uint32_t xcd_weights;      // rows-kernel split: (even << 16) | odd XCD weight, 0 = equal
+    int segment;               // split few large blocks / extents into segments (PRISKV_CRC_SEGMENT=0: off)
     uint32_t *d_lds_image[3];  // 64 KiB each: set B gap for G = 64, 32, 16
     uint32_t *d_fold;          // kFoldSets x 2048 words, set j for G = 1 << j
     uint32_t *d_nibrep[7];     // nibble fold tables for G = 1 << j (j >= 1), 8 x 16 x max(G, 32) words
     uint32_t *d_nib16;         // the extents kernel's: G = 16, width 16 (8 KiB)
     uint32_t *d_sarwate;       // 256 words
+    uint32_t *d_zpow;          // kZpowRows x 32 words: columns of Z_(2^k) (segment combine)
     uint32_t *d_rowshift;      // 16 x 4 x 32 words: columns of Z_-p o Z_(256(3-k)) (extents fold)
     // host-streamed path (guarded by lock)
     pthread_mutex_t lock;
@@ -151,10 +153,23 @@ constexpr int kAux = 2;   // cache policy of the streaming loads: nt
 constexpr int kExtRows = 2; // rows per chunk of the extents kernel (tools/ranges_explore)
 constexpr int kExtOpt = 3;  // extents kernel: nibble fold + row apply (bit 0), masks only where needed (bit 1)
 
-// extents through the row machinery (any base alignment, any lengths)
+constexpr int kZpowRows = 48;
+
+int launch_extents_seg(const priskv_crc_ctx *ctx, const uint8_t *base, uint64_t n, const uint64_t *offs,
+                       const uint32_t *lens, uint64_t stride, uint32_t len_const, uint32_t *out, hipStream_t s,
+                       uint64_t max_len, bool *used);
+
+// extents through the row machinery (any base alignment, any lengths).
+// max_len: the longest extent when the host knows it (0: unknown)
 int launch_extents(const priskv_crc_ctx *ctx, const uint8_t *base, uint64_t n, const uint64_t *offs,
-                   const uint32_t *lens, uint64_t stride, uint32_t len_const, uint32_t *out, hipStream_t s)
+                   const uint32_t *lens, uint64_t stride, uint32_t len_const, uint32_t *out, hipStream_t s,
+                   uint64_t max_len = 0)
 {
+    bool used = false;
+    if (int rc = launch_extents_seg(ctx, base, n, offs, lens, stride, len_const, out, s, max_len, &used))
+        return rc;
+    if (used)
+        return 0;
     const uint64_t shift = (uintptr_t)base & 15;
     const uint8_t *abase = base - shift;
     const uint64_t want = (n + kWaves - 1) / kWaves;
@@ -162,7 +177,7 @@ int launch_extents(const priskv_crc_ctx *ctx, const uint8_t *base, uint64_t n, c
     const uint32_t grid = (uint32_t)(want < cap ? want : cap);
     hipLaunchKernelGGL((crc_ranges_kernel<kExtRows, kNbuf, kAux, kExtOpt>), dim3(grid), dim3(kThreads), 0, s, abase,
                        n, offs, lens, shift, stride, len_const, ctx->d_lds_image[0], ctx->d_nib16, ctx->d_rowshift,
-                       out);
+                       out, nullptr, nullptr, nullptr, nullptr);
     return herr(hipGetLastError());
 }
 
@@ -268,6 +283,8 @@ uint32_t segments_for(const priskv_crc_ctx *ctx, uint64_t nblocks, uint32_t bs)
 {
     const uint64_t waves = (uint64_t)ctx->num_cus * kWaves; // 1 WG/CU: the plans for blocks > 16 KiB
     uint32_t S = 1;
+    if (!ctx->segment)
+        return S;
     while (!balanced(nblocks * S, waves) && bs / (2 * S) >= kMinSegment && (bs / (2 * S)) % PRV_ROW_BYTES == 0 &&
            bs % (2 * S) == 0)
         S *= 2;
@@ -276,6 +293,68 @@ uint32_t segments_for(const priskv_crc_ctx *ctx, uint64_t nblocks, uint32_t bs)
 
 int launch_rows_plain(const priskv_crc_ctx *ctx, const uint8_t *base, uint64_t nblocks, uint32_t bs, uint32_t *out,
                       hipStream_t s);
+
+// Few extents: the same kernel over segments of each extent.  The segments
+// are laid out on the device by crc_seg_plan_kernel (the host never sees
+// device-resident lengths); each segment's CRC is shifted to its extent's
+// end inside the extents kernel, and crc_seg_reduce_kernel XORs them.  The
+// segment-count cap per extent aims at about two segments per resident
+// wave; the scratch is stream-ordered like the rows path's.
+//
+// When.  The two extra launches and the scratch cost several us per call
+// (tools/bench_paths.py few): a loss for small values, which one wave
+// hashes in a few us, and a large win for big ones (one wave streams only
+// ~3.4 GB/s: 32 x 1 MiB 311 -> 23 us, 1 x 256 MiB 70.6 ms -> 97 us;
+// profiles/r01/few_values.jsonl).  When the host knows the longest extent
+// (one constant length on the blocks path, host arrays on the host scrub),
+// segment when the batch is unbalanced and that length is at least
+// kSegMinLen.  Device-resident lengths are unknown, so the rule uses the
+// count: at most kSegMaxExtents extents (an eighth of the resident waves).
+constexpr uint64_t kSegMaxExtents = 512;
+constexpr uint32_t kSegMinLen = 64u << 10;
+
+int launch_extents_seg(const priskv_crc_ctx *ctx, const uint8_t *base, uint64_t n, const uint64_t *offs,
+                       const uint32_t *lens, uint64_t stride, uint32_t len_const, uint32_t *out, hipStream_t s,
+                       uint64_t max_len, bool *used)
+{
+    const uint64_t waves = (uint64_t)ctx->num_cus * 2 * kWaves;
+    *used = false;
+    if (!offs)
+        max_len = len_const;
+    if (!ctx->segment || n == 0 || n > 64ull * kSegPlanPerLane)
+        return 0;
+    if (max_len ? (max_len < kSegMinLen || balanced(n, waves)) : n > kSegMaxExtents)
+        return 0;
+    uint32_t cap_log2 = 6;
+    while (cap_log2 < 10 && (n << cap_log2) < 2 * waves)
+        cap_log2++;
+    const size_t off_shift = ((n + 1) * 4 + 255) / 256 * 256;
+    const size_t off_sub = off_shift + (n + 255) / 256 * 256;
+    uint8_t *scr = nullptr;
+    if (int rc = herr(hipMallocAsync((void **)&scr, off_sub + (n << cap_log2) * 4, s)))
+        return rc;
+    uint32_t *prefix = reinterpret_cast<uint32_t *>(scr);
+    uint8_t *shifts = scr + off_shift;
+    uint32_t *sub = reinterpret_cast<uint32_t *>(scr + off_sub);
+    hipLaunchKernelGGL(crc_seg_plan_kernel, dim3(1), dim3(64), 0, s, offs ? lens : nullptr, len_const, n, cap_log2,
+                       prefix, shifts);
+    int rc = herr(hipGetLastError());
+    if (!rc) {
+        const uint64_t sh = (uintptr_t)base & 15;
+        hipLaunchKernelGGL((crc_ranges_kernel<kExtRows, kNbuf, kAux, kExtOpt | 4>), dim3(ctx->num_cus * 2),
+                           dim3(kThreads), 0, s, base - sh, n, offs, lens, sh, stride, len_const, ctx->d_lds_image[0],
+                           ctx->d_nib16, ctx->d_rowshift, out, prefix, shifts, ctx->d_zpow, sub);
+        rc = herr(hipGetLastError());
+    }
+    if (!rc) {
+        const uint32_t grid = (uint32_t)((n + 3) / 4);
+        hipLaunchKernelGGL(crc_seg_reduce_kernel, dim3(grid), dim3(256), 0, s, sub, prefix, n, out);
+        rc = herr(hipGetLastError());
+    }
+    const int frc = herr(hipFreeAsync(scr, s));
+    *used = true;
+    return rc ? rc : frc;
+}
 
 int launch_rows(const priskv_crc_ctx *ctx, const uint8_t *base, uint64_t nblocks, uint32_t bs, uint32_t *out,
                 hipStream_t s)
@@ -429,18 +508,27 @@ int priskv_crc_ctx_create(int device, priskv_crc_ctx **out)
         goto fail;
     c->max_wgs = 2 * c->num_cus;
     c->xcd_weights = xcd_weights(c->num_cus);
+    {
+        const char *e = getenv("PRISKV_CRC_SEGMENT");
+        c->segment = !(e && !strcmp(e, "0"));
+    }
     for (int j = 0; j < kFoldSets; j++)
         prv_fold_columns(h_fold + j * 2048, 1u << j);
     prv_sarwate_table(h_sar);
     if ((rc = herr(hipMalloc((void **)&c->d_fold, sizeof(uint32_t) * 2048 * kFoldSets))) ||
         (rc = herr(hipMalloc((void **)&c->d_sarwate, sizeof(h_sar)))) ||
-        (rc = herr(hipMalloc((void **)&c->d_rowshift, sizeof(uint32_t) * 16 * 4 * 32))))
+        (rc = herr(hipMalloc((void **)&c->d_rowshift, sizeof(uint32_t) * 16 * 4 * 32))) ||
+        (rc = herr(hipMalloc((void **)&c->d_zpow, sizeof(uint32_t) * kZpowRows * 32))))
         goto fail;
     if ((rc = herr(hipMemcpy(c->d_fold, h_fold, sizeof(uint32_t) * 2048 * kFoldSets, hipMemcpyHostToDevice))) ||
         (rc = herr(hipMemcpy(c->d_sarwate, h_sar, sizeof(h_sar), hipMemcpyHostToDevice))))
         goto fail;
     prv_rowshift_columns(h_img);
     if ((rc = herr(hipMemcpy(c->d_rowshift, h_img, sizeof(uint32_t) * 16 * 4 * 32, hipMemcpyHostToDevice))))
+        goto fail;
+    for (int k = 0; k < kZpowRows; k++)
+        prv_shift_columns(h_img + k * 32, 1ull << k);
+    if ((rc = herr(hipMemcpy(c->d_zpow, h_img, sizeof(uint32_t) * kZpowRows * 32, hipMemcpyHostToDevice))))
         goto fail;
     for (int gi = 0; gi < 3; gi++) {
         const uint32_t G = 64u >> gi; // 64, 32, 16
@@ -498,6 +586,7 @@ void priskv_crc_ctx_destroy(priskv_crc_ctx *c)
     (void)hipFree(c->d_fold);
     (void)hipFree(c->d_sarwate);
     (void)hipFree(c->d_rowshift);
+    (void)hipFree(c->d_zpow);
     (void)hipFree(c->d_scrub);
     if (c->aux)
         (void)hipStreamDestroy(c->aux);
@@ -522,8 +611,9 @@ int priskv_crc32_blocks_dev(const priskv_crc_ctx *ctx, const void *d_base, uint6
     return launch_blocks(ctx, (const uint8_t *)d_base, nblocks, block_size, d_out, (hipStream_t)stream);
 }
 
-int priskv_crc32_ranges_dev(const priskv_crc_ctx *ctx, const void *d_base, const uint64_t *d_offsets,
-                            const uint32_t *d_lengths, uint64_t n, uint32_t *d_out, void *stream)
+namespace {
+int ranges_dev(const priskv_crc_ctx *ctx, const void *d_base, const uint64_t *d_offsets, const uint32_t *d_lengths,
+               uint64_t n, uint32_t *d_out, hipStream_t stream, uint64_t max_len)
 {
     if (!ctx)
         return -EINVAL;
@@ -534,7 +624,14 @@ int priskv_crc32_ranges_dev(const priskv_crc_ctx *ctx, const void *d_base, const
     DevGuard g(ctx->device);
     if (!g.ok)
         return -ENODEV;
-    return launch_extents(ctx, (const uint8_t *)d_base, n, d_offsets, d_lengths, 0, 0, d_out, (hipStream_t)stream);
+    return launch_extents(ctx, (const uint8_t *)d_base, n, d_offsets, d_lengths, 0, 0, d_out, stream, max_len);
+}
+} // namespace
+
+int priskv_crc32_ranges_dev(const priskv_crc_ctx *ctx, const void *d_base, const uint64_t *d_offsets,
+                            const uint32_t *d_lengths, uint64_t n, uint32_t *d_out, void *stream)
+{
+    return ranges_dev(ctx, d_base, d_offsets, d_lengths, n, d_out, (hipStream_t)stream, 0);
 }
 
 int priskv_crc32_verify_dev(const priskv_crc_ctx *ctx, const void *d_base, const uint64_t *d_offsets,
@@ -615,9 +712,12 @@ int priskv_crc32_ranges_host(priskv_crc_ctx *ctx, const void *h_base, uint64_t r
         return 0;
     if (!h_base || !h_offsets || !h_lengths || !h_out || !region_bytes)
         return -EINVAL;
-    for (uint64_t i = 0; i < n; i++)
+    uint64_t max_len = 1; // known (>= 1): lets launch_extents decide segmentation from the sizes
+    for (uint64_t i = 0; i < n; i++) {
         if (h_offsets[i] > region_bytes || h_lengths[i] > region_bytes - h_offsets[i])
             return -EINVAL;
+        max_len = h_lengths[i] > max_len ? h_lengths[i] : max_len;
+    }
     DevGuard g(ctx->device);
     if (!g.ok)
         return -ENODEV;
@@ -652,7 +752,7 @@ int priskv_crc32_ranges_host(priskv_crc_ctx *ctx, const void *h_base, uint64_t r
         uint32_t *d_crc = d_len + n;
         if (!(rc = herr(hipMemcpyAsync(d_off, h_offsets, n * 8, hipMemcpyHostToDevice, ctx->aux))) &&
             !(rc = herr(hipMemcpyAsync(d_len, h_lengths, n * 4, hipMemcpyHostToDevice, ctx->aux))) &&
-            !(rc = priskv_crc32_ranges_dev(ctx, dptr, d_off, d_len, n, d_crc, ctx->aux)) &&
+            !(rc = ranges_dev(ctx, dptr, d_off, d_len, n, d_crc, ctx->aux, max_len)) &&
             !(rc = herr(hipMemcpyAsync(h_out, d_crc, n * 4, hipMemcpyDeviceToHost, ctx->aux))))
             rc = herr(hipStreamSynchronize(ctx->aux));
         else

@@ -33,6 +33,30 @@ def ctx(torch_cuda):
     c.close()
 
 
+@pytest.fixture(scope="module")
+def ctx_noseg(torch_cuda):
+    """A context with segmentation off (PRISKV_CRC_SEGMENT=0, read at creation):
+    every call takes the one-wave-per-extent / unsegmented rows path."""
+    import os
+    from priskv_amd import CrcContext
+    old = os.environ.get("PRISKV_CRC_SEGMENT")
+    os.environ["PRISKV_CRC_SEGMENT"] = "0"
+    try:
+        c = CrcContext(0)
+    finally:
+        if old is None:
+            del os.environ["PRISKV_CRC_SEGMENT"]
+        else:
+            os.environ["PRISKV_CRC_SEGMENT"] = old
+    yield c
+    c.close()
+
+
+@pytest.fixture(params=["segmented", "unsegmented"])
+def any_ctx(request, ctx, ctx_noseg):
+    return ctx if request.param == "segmented" else ctx_noseg
+
+
 def _region(torch, ctx, nbytes, seed=SEED, word_offset=0, pad=0):
     t = torch.empty(nbytes + pad + 16, dtype=torch.uint8, device="cuda")
     ctx.fill_splitmix(t, seed, word_offset, nbytes=nbytes + pad)
@@ -147,7 +171,8 @@ def test_single_bit_flips_detected(torch_cuda, ctx):
     assert {i for i in range(nb) if out[i] != base[i]} <= touched
 
 
-def test_ranges_vs_oracle(torch_cuda, ctx):
+def test_ranges_vs_oracle(torch_cuda, any_ctx):
+    ctx = any_ctx
     torch = torch_cuda
     n = 8 << 20
     t = _region(torch, ctx, n, SEED, 99)
@@ -163,10 +188,11 @@ def test_ranges_vs_oracle(torch_cuda, ctx):
     assert np.array_equal(_u32(out), want)
 
 
-def test_ranges_edges(torch_cuda, ctx):
+def test_ranges_edges(torch_cuda, any_ctx):
     """Extents at every 16-B phase, lengths around 16 / 1 KiB boundaries, ranges
     starting at byte 0 (rows right-aligned before the region start) and ranges
     ending exactly at the end of an exactly-sized allocation."""
+    ctx = any_ctx
     torch = torch_cuda
     n = 1 << 16
     t = torch.empty(n, dtype=torch.uint8, device="cuda")  # no padding after the end
@@ -198,10 +224,11 @@ def test_ranges_edges(torch_cuda, ctx):
     assert np.array_equal(_u32(out2), O.crc32_ranges(view.cpu().numpy(), o2, l2))
 
 
-def test_ranges_chunk_boundaries(torch_cuda, ctx):
+def test_ranges_chunk_boundaries(torch_cuda, any_ctx):
     """Extents whose row count crosses the extents kernel's 4-row chunk edges
     (lengths m*4 KiB +- 0..17 at every 16-B start phase): leading virtual rows,
     the trailing pad p = 0..15 undone by Z_-p, and head + tail masks in one row."""
+    ctx = any_ctx
     torch = torch_cuda
     n = 1 << 17
     t = torch.empty(n, dtype=torch.uint8, device="cuda")
@@ -232,6 +259,36 @@ def test_segmented_large_blocks(torch_cuda, ctx, bs, nb):
     torch.cuda.synchronize()
     want = O.crc32_blocks(t[: bs * nb].cpu().numpy(), bs, nthreads=8)
     assert np.array_equal(_u32(out), want), (bs, nb)
+
+
+@pytest.mark.parametrize("lens", [[64 << 20], [(1 << 20) + 5, 16 << 20, 0, 17], [1 << 20] * 32,
+                                  [(4 << 20) - 1] * 3 + [12345] * 50, [1 << 14] * 7 + [(1 << 14) + 1] * 7,
+                                  [(1 << 24) + (1 << 20)] * 2,
+                                  [0, 1, 15, 16, 17, 1023, 1024, 1025, 16383, 16384, 16385, 65535, 65536, 65537]
+                                  + list(np.random.default_rng(9).integers(0, 300000, 498))])
+def test_few_large_extents(torch_cuda, ctx, ctx_noseg, lens):
+    """Fewer extents than the resident waves: segmented on the device
+    (crc_seg_plan / segment CRCs / crc_seg_combine); must equal the
+    one-wave-per-extent path and the oracle, at ragged offsets."""
+    torch = torch_cuda
+    lens = np.array(lens, dtype=np.uint32)
+    rng = np.random.default_rng(int(lens.sum()) & 0xFFFF)
+    n = int(lens.sum()) + 4096 * len(lens) + 4096
+    t = _region(torch, ctx, n, SEED ^ 0x77, 3)
+    offs, pos = [], 0
+    for ln in lens:
+        pos += int(rng.integers(0, 4096))
+        offs.append(pos)
+        pos += int(ln)
+    o = np.array(offs, dtype=np.uint64)
+    d_o = torch.from_numpy(o.astype(np.int64)).cuda()
+    d_l = torch.from_numpy(lens.view(np.int32)).cuda()
+    got = _u32(ctx.ranges_dev(t, d_o, d_l))
+    ref = _u32(ctx_noseg.ranges_dev(t, d_o, d_l))
+    torch.cuda.synchronize()
+    want = O.crc32_ranges(t[:n].cpu().numpy(), o, lens)
+    assert np.array_equal(ref, want)
+    assert np.array_equal(got, want)
 
 
 def test_verify_dev(torch_cuda, ctx):

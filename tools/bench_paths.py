@@ -90,6 +90,37 @@ def ranges_dev_case(ctx, bs=4096, region=4 << 30, n=1 << 19, steps=10):
     del t, host
 
 
+def few_values_case(ctx, ctx_noseg):
+    """Fewer values than resident waves (a GET batch to verify, a few huge
+    values): device-segmented extents against one wave per value, same
+    process, wall time per call including the plan and combine launches."""
+    rng = np.random.default_rng(3)
+    for count, ln in ((1, 256 << 20), (8, 16 << 20), (32, 1 << 20), (32, 4 << 20), (256, 1 << 20),
+                      (1000, 64 << 10), (3000, 64 << 10), (32, 4096 * 4 - 100)):
+        region = count * (ln + 4096) + 4096
+        t = torch.empty(region, dtype=torch.uint8, device="cuda")
+        ctx.fill_splitmix(t, SEED, 0)
+        offs = (np.arange(count, dtype=np.uint64) * (ln + 4096) + rng.integers(0, 4096, count).astype(np.uint64))
+        lens = np.full(count, ln, dtype=np.uint32)
+        d_o = torch.from_numpy(offs.astype(np.int64)).cuda()
+        d_l = torch.from_numpy(lens.view(np.int32)).cuda()
+        res = {}
+        outs = {}
+        for name, c in (("segmented", ctx), ("one_wave_per_value", ctx_noseg)):
+            out = torch.empty(count, dtype=torch.int32, device="cuda")
+            sec = timeit(lambda: c.ranges_dev(t, d_o, d_l, out=out), 20)
+            res[name] = (round(sec * 1e6, 1), round(count * ln / sec / 2**30, 1))
+            outs[name] = as_u32(out)
+        k = min(count, 8)
+        want = O.crc32_ranges(t.cpu().numpy(), offs[:k], lens[:k])
+        ok = np.array_equal(outs["segmented"], outs["one_wave_per_value"]) and np.array_equal(
+            outs["segmented"][:k], want)
+        emit(path="ranges_dev_few", values=count, value_len=ln, segmented_us=res["segmented"][0],
+             segmented_GiBs=res["segmented"][1], unsegmented_us=res["one_wave_per_value"][0],
+             unsegmented_GiBs=res["one_wave_per_value"][1], bit_exact=bool(ok))
+        del t
+
+
 def ranges_host_case(ctx, bs=4096, region=2 << 30, n=1 << 17):
     rng = np.random.default_rng(2)
     host = O.fill_splitmix(region, SEED, 0)
@@ -179,6 +210,12 @@ def main():
             blocks_case(ctx, bs, total)
     if "ranges" in which:
         ranges_dev_case(ctx)
+    if "few" in which or "ranges" in which:
+        os.environ["PRISKV_CRC_SEGMENT"] = "0"
+        ctx_noseg = CrcContext(0)
+        del os.environ["PRISKV_CRC_SEGMENT"]
+        few_values_case(ctx, ctx_noseg)
+        ctx_noseg.close()
     if "host" in which:
         ranges_host_case(ctx)
         blocks_host_case(ctx)

@@ -1,0 +1,8 @@
+# device-segmented extents: parity (segmented and unsegmented contexts), few-values timing
+set -e
+R=$GRAFT_REPO_ROOT
+O=$R/gpurun_out/r1zw
+mkdir -p $O
+timeout -k 10 600 python -u -m pytest tests -x -v -m gpu --timeout 300 --timeout-method thread > $O/pytest.log 2>&1
+timeout -k 10 400 python tools/bench_paths.py few > $O/few.jsonl 2> $O/few.err
+echo ALLDONE

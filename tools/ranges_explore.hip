@@ -52,14 +52,14 @@ struct Variant {
             [](dim3 g, const uint8_t *b, uint64_t n, const uint64_t *o, const uint32_t *l, uint64_t stride,       \
                uint32_t lc, const uint32_t *img, const uint32_t *fold, const uint32_t *un, uint32_t *out) {       \
                 hipLaunchKernelGGL((crc_ranges_kernel<CH, NB, AUX>), g, dim3(kThreads), 0, 0, b, n, o, l, 0ull,   \
-                                   stride, lc, img, fold, un, out);                                                \
+                                   stride, lc, img, fold, un, out, nullptr, nullptr, nullptr, nullptr);                              \
             }, false}
 #define RV2(CH, NB, AUX, WG)                                                                                   \
     Variant{"ext2 CH" #CH " NBUF" #NB " AUX" #AUX " wg/cu" #WG, WG,                                            \
             [](dim3 g, const uint8_t *b, uint64_t n, const uint64_t *o, const uint32_t *l, uint64_t stride,       \
                uint32_t lc, const uint32_t *img, const uint32_t *fold, const uint32_t *un, uint32_t *out) {       \
                 hipLaunchKernelGGL((crc_ranges2_kernel<CH, NB, AUX>), g, dim3(kThreads), 0, 0, b, n, o, l, 0ull,  \
-                                   stride, lc, img, fold, un, out);                                                \
+                                   stride, lc, img, fold, un, out, nullptr, nullptr, nullptr, nullptr);                              \
             }, true}
 
 // OPT bit 0 (nibble fold) takes its two images from these globals
@@ -70,7 +70,7 @@ static uint32_t *g_nib16 = nullptr, *g_rowshift = nullptr;
                uint32_t lc, const uint32_t *img, const uint32_t *fold, const uint32_t *un, uint32_t *out) {       \
                 hipLaunchKernelGGL((crc_ranges_kernel<CH, NB, AUX, OPT>), g, dim3(kThreads), 0, 0, b, n, o, l,     \
                                    0ull, stride, lc, img, ((OPT) & 1) ? g_nib16 : fold,                           \
-                                   ((OPT) & 1) ? g_rowshift : un, out);                                           \
+                                   ((OPT) & 1) ? g_rowshift : un, out, nullptr, nullptr, nullptr, nullptr);                         \
             }, false}
 
 struct Set {
