@@ -162,9 +162,15 @@ void prv_shift_columns(uint32_t out[32], uint64_t nbytes)
 
 void prv_lds_image(uint32_t out[PRV_LDS_WORDS], uint32_t gap_bytes)
 {
+    prv_lds_image_step(out, 4, gap_bytes);
+}
+
+void prv_lds_image_step(uint32_t out[PRV_LDS_WORDS], uint32_t step, uint32_t gap_bytes)
+{
+    /* as prv_lds_image with Z_step / Z_(step+gap) (step 8: slice-by-8 pairs) */
     uint32_t za[32], zb[32];
-    prv_shift_columns(za, 4);
-    prv_shift_columns(zb, 4 + (uint64_t)gap_bytes);
+    prv_shift_columns(za, step);
+    prv_shift_columns(zb, step + (uint64_t)gap_bytes);
     for (uint32_t idx = 0; idx < 256; idx++)
         for (uint32_t k = 0; k < 8; k++)
             for (uint32_t t = 0; t < 4; t++) {

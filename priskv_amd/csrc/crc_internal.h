@@ -21,6 +21,7 @@ extern "C"
 #define PRV_ROW_GAP (PRV_ROW_BYTES - 16u)
 
 PRV_HIDDEN void prv_lds_image(uint32_t out[PRV_LDS_WORDS], uint32_t gap_bytes);
+PRV_HIDDEN void prv_lds_image_step(uint32_t out[PRV_LDS_WORDS], uint32_t step, uint32_t gap_bytes);
 PRV_HIDDEN void prv_fold_columns(uint32_t out[32 * 64], uint32_t group);
 /* nibble fold tables, 8*16*width words (crc_device.inc nib_fold) */
 PRV_HIDDEN void prv_fold_nibbles(uint32_t *out, uint32_t group, uint32_t width);

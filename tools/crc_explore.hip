@@ -26,11 +26,14 @@ namespace {
 #include "crc_pair_explore.inc"
 
 // read-only roof with the rows kernel's loop and addressing (same loads, no hashing)
-template <int G, int CH, int NBUF, int AUX>
+// TIMING: also write each wave's start / end s_memrealtime after the sink
+// words (as crc_rows_kernel's OPT bit 3)
+template <int G, int CH, int NBUF, int AUX, bool TIMING = false>
 __global__ __launch_bounds__(kThreads, rows_min_wg(CH, NBUF)) void roof_rows(const uint8_t *__restrict__ base, uint64_t ngroups,
                                                          uint32_t block_size, const uint32_t *, const uint32_t *,
                                                          uint32_t *__restrict__ out, uint32_t xw)
 {
+    const uint64_t t_start = TIMING ? __builtin_amdgcn_s_memrealtime() : 0;
     constexpr int NB = 64 / G, RB = 16 * G;
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -86,6 +89,11 @@ __global__ __launch_bounds__(kThreads, rows_min_wg(CH, NBUF)) void roof_rows(con
             acc ^= buf[j][k].x ^ buf[j][k].y ^ buf[j][k].z ^ buf[j][k].w;
     }
     out[wid * 64 + lane] = acc;
+    if (TIMING && lane == 0) {
+        const uint64_t t_end = __builtin_amdgcn_s_memrealtime();
+        out[ngroups * (64 / G) + 2 * wid] = (uint32_t)t_start;
+        out[ngroups * (64 / G) + 2 * wid + 1] = (uint32_t)t_end;
+    }
 }
 
 __global__ __launch_bounds__(256) void roof_gridstride(const v4u *__restrict__ p, uint64_t n16,
@@ -215,8 +223,29 @@ static uint32_t g_epoch = 0;
                                    (uint32_t)(((WE) << 16) | (WO)));                                       \
             }, {}}
 #define ROOF_VARIANT(G, CH, NB, AUX, WGPC) ROOF_VARIANT_W(G, CH, NB, AUX, WGPC, 0, 0)
+// roof with per-wave timing: writes into the CRC output buffer (is_crc for
+// the buffer choice, opt 8 for the timing report; excluded from the
+// bit-identity check by the is_crc/opt logic below)
+#define ROOF_T_VARIANT(G, CH, NB, AUX, WGPC, WE, WO)                                                       \
+    Variant{"rooft G" #G " CH" #CH " NBUF" #NB " AUX" #AUX " wg/cu" #WGPC " xw" #WE ":" #WO, true, G, CH,     \
+            WGPC, 8 | 4,                                                                                   \
+            [](dim3 g, hipStream_t s, const uint8_t *b, uint64_t n, uint32_t bs, const uint32_t *img,       \
+               const uint32_t *fold, uint32_t *o) {                                                        \
+                hipLaunchKernelGGL((roof_rows<G, CH, NB, AUX, true>), g, dim3(kThreads), 0, s, b, n, bs, img, fold, \
+                                   o, (uint32_t)(((WE) << 16) | (WO)));                                    \
+            }, {}}
 // nibble-table fold (OPT bit 5): the fold pointer is the nibble image
 static uint32_t *g_nib[65] = {};
+// slice-by-8 pairs (OPT bit 6): 128 KiB image [Z_4 sets | Z_8 sets]
+static uint32_t *g_img8[65] = {};
+#define S8_VARIANT_W(G, CH, NB, AUX, WGPC, OPT, WE, WO)                                                       \
+    Variant{"s8 G" #G " CH" #CH " NBUF" #NB " AUX" #AUX " wg/cu" #WGPC " opt" #OPT " xw" #WE ":" #WO, true, G,  \
+            CH, WGPC, OPT,                                                                                     \
+            [](dim3 g, hipStream_t s, const uint8_t *b, uint64_t n, uint32_t bs, const uint32_t *,              \
+               const uint32_t *, uint32_t *o) {                                                                \
+                hipLaunchKernelGGL((crc_rows_kernel<G, CH, NB, AUX, (OPT) | 32 | 64>), g, dim3(kThreads), 0, s, b, n, \
+                                   bs, g_img8[G], g_nib[G], o, (uint32_t)(((WE) << 16) | (WO)));               \
+            }, {}}
 #define NIB_VARIANT_W(G, CH, NB, AUX, WGPC, OPT, WE, WO)                                                      \
     Variant{"nib G" #G " CH" #CH " NBUF" #NB " AUX" #AUX " wg/cu" #WGPC " opt" #OPT " xw" #WE ":" #WO, true, G, \
             CH, WGPC, OPT,                                                                                     \
@@ -326,6 +355,11 @@ int main(int argc, char **argv)
         CK(hipMemcpy(d_img[G], img.data(), img.size() * 4, hipMemcpyHostToDevice));
         CK(hipMemcpy(d_fold[G], fold.data(), fold.size() * 4, hipMemcpyHostToDevice));
         CK(hipMemcpy(g_nib[G], nib.data(), nib.size() * 4, hipMemcpyHostToDevice));
+        std::vector<uint32_t> img8(2 * PRV_LDS_WORDS);
+        prv_lds_image_step(img8.data(), 4, 16u * G - 16u);
+        prv_lds_image_step(img8.data() + PRV_LDS_WORDS, 8, 16u * G - 16u);
+        CK(hipMalloc(&g_img8[G], img8.size() * 4));
+        CK(hipMemcpy(g_img8[G], img8.data(), img8.size() * 4, hipMemcpyHostToDevice));
     }
     if (bs <= 512)
         return small_ab(bs, nb, rounds, ncu);
@@ -344,6 +378,13 @@ int main(int argc, char **argv)
     // first entry = product reference for the bit-exact cross-check and the sustained run
     all.push_back(CRC_VARIANT_W(32, 8, 2, 2, 1, 2, 31, 29));
     all.push_back(NIB_VARIANT_W(32, 8, 2, 2, 1, 2, 31, 29));
+    all.push_back(S8_VARIANT_W(32, 8, 2, 2, 1, 2, 31, 29));
+    all.push_back(ROOF_T_VARIANT(32, 8, 2, 2, 1, 31, 29));
+    all.push_back(ROOF_T_VARIANT(32, 8, 2, 2, 1, 0, 0));
+    all.push_back(NIB_VARIANT_W(32, 8, 2, 2, 1, 10, 31, 29));
+    all.push_back(NIB_VARIANT_W(32, 8, 2, 2, 1, 10, 0, 0));
+    all.push_back(S8_VARIANT_W(32, 8, 2, 2, 1, 6, 31, 29));
+    all.push_back(S8_VARIANT_W(32, 8, 3, 2, 1, 2, 31, 29));
     all.push_back(NIB_VARIANT_W(32, 8, 3, 2, 1, 2, 31, 29));
     all.push_back(NIB_VARIANT_W(32, 8, 2, 2, 2, 2, 31, 29));
     all.push_back(NIB_VARIANT_W(32, 8, 2, 2, 1, 6, 31, 29));
