@@ -498,6 +498,57 @@ def test_stream_argument(torch_cuda, ctx):
     assert np.array_equal(_u32(out), O.crc32_blocks(t.cpu().numpy()[: bs * nb], bs, nthreads=8))
 
 
+def test_concurrent_streams_and_threads(torch_cuda, ctx):
+    """One context shared by 4 host threads, each on its own stream, each
+    mixing calls that need stream-ordered scratch (segmented extents, segmented
+    large blocks) with plain ones; every result must equal the oracle's
+    (contexts are immutable, *_dev calls may run concurrently)."""
+    import threading
+    torch = torch_cuda
+    region = _region(torch, ctx, 48 << 20, SEED ^ 0xC0, 1)
+    torch.cuda.synchronize()
+    host = region[: 48 << 20].cpu().numpy()
+    rng = np.random.default_rng(12)
+    jobs = []
+    for k in range(4):
+        lens = rng.integers(1, 4 << 20, 6).astype(np.uint32)
+        offs = np.array([rng.integers(0, (48 << 20) - int(ln)) for ln in lens], dtype=np.uint64)
+        jobs.append((offs, lens, 1 << 20, 3 + k))
+    want = [(O.crc32_ranges(host, o, ln), O.crc32_blocks(host[: bs * nb], bs, nthreads=4),
+             O.crc32_blocks(host[:4096 * 1000], 4096, nthreads=4)) for o, ln, bs, nb in jobs]
+    got = [None] * len(jobs)
+    errs = []
+
+    def run(k):
+        try:
+            o, ln, bs, nb = jobs[k]
+            s = torch.cuda.Stream()
+            with torch.cuda.stream(s):  # inputs copied on the stream that reads them
+                d_o = torch.from_numpy(o.astype(np.int64)).cuda()
+                d_l = torch.from_numpy(ln.view(np.int32)).cuda()
+            res = []
+            for _ in range(5):
+                with torch.cuda.stream(s):
+                    a = ctx.ranges_dev(region, d_o, d_l, stream=s)
+                    b = ctx.blocks_dev(region, bs, nblocks=nb, stream=s)
+                    c = ctx.blocks_dev(region, 4096, nblocks=1000, stream=s)
+                s.synchronize()
+                res.append((_u32(a), _u32(b), _u32(c)))
+            got[k] = res
+        except Exception as e:  # surfaced below
+            errs.append(e)
+
+    th = [threading.Thread(target=run, args=(k,)) for k in range(len(jobs))]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert not errs, errs
+    for k in range(len(jobs)):
+        for a, b, c in got[k]:
+            assert np.array_equal(a, want[k][0]) and np.array_equal(b, want[k][1]) and np.array_equal(c, want[k][2])
+
+
 def test_bad_args_on_gpu(torch_cuda, ctx):
     from priskv_amd.crc import lib
     L = lib()
