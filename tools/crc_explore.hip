@@ -24,6 +24,7 @@ namespace {
 #include "../priskv_amd/csrc/crc_device.inc"
 #include "crc_dyn_explore.inc"
 #include "crc_pair_explore.inc"
+#include "crc_tail_explore.inc"
 
 // read-only roof with the rows kernel's loop and addressing (same loads, no hashing)
 // TIMING: also write each wave's start / end s_memrealtime after the sink
@@ -199,6 +200,19 @@ static uint32_t *g_ctr = nullptr;
                 hipLaunchKernelGGL((crc_rows_dyn_kernel<G, CH, NB, AUX, OPT>), g, dim3(kThreads), 0, s, b, n, bs, \
                                    img, fold, o, g_ctr);                                                       \
             }, {}}
+// static head + per-XCD pooled tail (crc_tail_explore.inc): TS groups per
+// tile, K tiles per wave pooled; counters zeroed on the stream before each launch
+#define TAIL_VARIANT(G, CH, NB, AUX, OPT, WE, WO, TS, K)                                                       \
+    Variant{((OPT) & 16 ? "roof tail G" #G " CH" #CH " NBUF" #NB " ts" #TS " k" #K " xw" #WE ":" #WO          \
+                        : "crc tail G" #G " CH" #CH " NBUF" #NB " opt" #OPT " ts" #TS " k" #K " xw" #WE ":" #WO), \
+            !((OPT) & 16), G, CH, 1, -1,                                                                       \
+            [](dim3 g, hipStream_t s, const uint8_t *b, uint64_t n, uint32_t bs, const uint32_t *img,           \
+               const uint32_t *fold, uint32_t *o) {                                                            \
+                (void)hipMemsetAsync(g_ctr, 0, 4096, s);                                                       \
+                hipLaunchKernelGGL((crc_rows_tail_kernel<G, CH, NB, AUX, OPT>), g, dim3(kThreads), 0, s, b, n, bs, \
+                                   img, ((OPT) & 32) ? g_nib[G] : fold, o, (uint32_t)(((WE) << 16) | (WO)), g_ctr, \
+                                   (uint32_t)(TS), (uint32_t)(K));                                             \
+            }, {}}
 // paired (forward / backward wave pairs; NEGATIVE RESULT, explorer only --
 // profiles/r01/explore_4k_pair.log: per-XCD finish times equalize, but both
 // the CRC and the read roof lose 2-4 %): slots + epoch via globals
@@ -371,7 +385,7 @@ int main(int argc, char **argv)
                        0ull);
     CK(hipDeviceSynchronize());
 
-    CK(hipMalloc(&g_ctr, 64));
+    CK(hipMalloc(&g_ctr, 4096));
     CK(hipMalloc(&g_slots, (size_t)ncu * 2 * kWaves * 128));
     CK(hipMemset(g_slots, 0, (size_t)ncu * 2 * kWaves * 128));
     std::vector<Variant> all;
@@ -379,6 +393,14 @@ int main(int argc, char **argv)
     all.push_back(CRC_VARIANT_W(32, 8, 2, 2, 1, 2, 31, 29));
     all.push_back(NIB_VARIANT_W(32, 8, 2, 2, 1, 2, 31, 29));
     all.push_back(S8_VARIANT_W(32, 8, 2, 2, 1, 2, 31, 29));
+    all.push_back(TAIL_VARIANT(32, 8, 2, 2, 34, 31, 29, 8, 4));
+    all.push_back(TAIL_VARIANT(32, 8, 2, 2, 34, 31, 29, 4, 8));
+    all.push_back(TAIL_VARIANT(32, 8, 2, 2, 34, 31, 29, 16, 4));
+    all.push_back(TAIL_VARIANT(32, 8, 2, 2, 34, 31, 29, 8, 8));
+    all.push_back(TAIL_VARIANT(32, 8, 2, 2, 34, 0, 0, 8, 4));
+    all.push_back(TAIL_VARIANT(32, 8, 2, 2, 34, 0, 0, 8, 8));
+    all.push_back(TAIL_VARIANT(32, 8, 2, 2, 16, 31, 29, 8, 4));
+    all.push_back(TAIL_VARIANT(64, 4, 2, 2, 0, 31, 29, 4, 4));
     all.push_back(ROOF_T_VARIANT(32, 8, 2, 2, 1, 31, 29));
     all.push_back(ROOF_T_VARIANT(32, 8, 2, 2, 1, 0, 0));
     all.push_back(NIB_VARIANT_W(32, 8, 2, 2, 1, 10, 31, 29));
