@@ -134,6 +134,16 @@ def host_unregister(arr: np.ndarray) -> None:
 
 
 # ---------------------------------------------------------------- context
+def _device_args(region, *tensors) -> None:
+    """The C ABI takes raw device pointers: a host tensor, another device or a
+    strided view would be read as garbage (or fault), so refuse them here."""
+    if not region.is_cuda:
+        raise ValueError("region must be a device tensor (use the *_host calls for host memory)")
+    for t in tensors:
+        if not t.is_cuda or t.device != region.device or not t.is_contiguous():
+            raise ValueError("offsets / lengths / out must be contiguous tensors on the region's device")
+
+
 def _stream_ptr(stream) -> Optional[int]:
     if stream is None:
         import torch
@@ -198,6 +208,9 @@ class CrcContext:
             raise ValueError("offsets must be int64 and lengths int32 device tensors of equal length")
         if out is None:
             out = torch.empty(n, dtype=torch.int32, device=region.device)
+        if out.numel() < n or out.element_size() != 4:
+            raise ValueError("out must be a 4-byte tensor of >= len(offsets) entries")
+        _device_args(region, offsets, lengths, out)
         _check(lib().priskv_crc32_ranges_dev(self._h, region.data_ptr(), offsets.data_ptr(),
                                              lengths.data_ptr(), n, out.data_ptr(), _stream_ptr(stream)),
                "priskv_crc32_ranges_dev")
@@ -214,13 +227,20 @@ class CrcContext:
             raise ValueError("offsets int64, lengths int32 and expected 4-byte device tensors of equal length")
         if status is None:
             status = torch.empty(2, dtype=torch.int64, device=region.device)
+        if status.numel() < 2 or status.element_size() != 8:
+            raise ValueError("status must be an 8-byte tensor of >= 2 entries")
+        _device_args(region, offsets, lengths, expected, status)
         _check(lib().priskv_crc32_verify_dev(self._h, region.data_ptr(), offsets.data_ptr(), lengths.data_ptr(),
                                              n, expected.data_ptr(), status.data_ptr(), _stream_ptr(stream)),
                "priskv_crc32_verify_dev")
         return status
 
     def fill_splitmix(self, region, seed: int, word_offset: int = 0, stream=None, nbytes=None) -> None:
-        nb = region.numel() * region.element_size() if nbytes is None else nbytes
+        size = region.numel() * region.element_size()
+        nb = size if nbytes is None else nbytes
+        if nb > size:
+            raise ValueError("nbytes exceeds the region")
+        _device_args(region)
         _check(lib().priskv_crc_fill_splitmix_dev(self._h, region.data_ptr(), nb, seed & (2**64 - 1),
                                                   word_offset, _stream_ptr(stream)),
                "priskv_crc_fill_splitmix_dev")

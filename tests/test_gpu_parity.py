@@ -558,6 +558,20 @@ def test_bad_args_on_gpu(torch_cuda, ctx):
     import ctypes
     h = ctypes.c_void_p()
     assert L.priskv_crc_ctx_create(4096, ctypes.byref(h)) == -19
+    # the binding refuses host or strided pointer arguments before they reach a kernel
+    torch = torch_cuda
+    t = torch.zeros(1 << 16, dtype=torch.uint8, device="cuda")
+    o = torch.zeros(4, dtype=torch.int64)
+    ln = torch.full((4,), 16, dtype=torch.int32)
+    for bad in ((o, ln.cuda()), (o.cuda(), ln), (o.cuda()[::2], ln.cuda()[::2])):
+        with pytest.raises(ValueError):
+            ctx.ranges_dev(t, *bad)
+    with pytest.raises(ValueError):
+        ctx.verify_dev(t, o.cuda(), ln.cuda(), torch.zeros(4, dtype=torch.int32))
+    with pytest.raises(ValueError):
+        ctx.fill_splitmix(t, 1, nbytes=(1 << 16) + 1)
+    with pytest.raises(ValueError):
+        ctx.ranges_dev(t.cpu(), o.cuda(), ln.cuda())
 
 
 @pytest.mark.slow
