@@ -43,8 +43,10 @@ extern "C"
 typedef struct priskv_crc_ctx priskv_crc_ctx;
 
 /* Create a context on HIP device `device`: uploads the CRC tables (64 KiB
- * LDS image + fold/shift matrices) and sizes the persistent grid from the
- * device's CU count.  *out is set only on success. */
+ * LDS images, nibble fold tables, shift matrices) and sizes the persistent
+ * grid from the device's CU count.  *out is set only on success.
+ * PRISKV_CRC_SEGMENT=0 in the environment at creation turns off the
+ * segmentation of few large blocks / extents (measurement only). */
 int priskv_crc_ctx_create(int device, priskv_crc_ctx **out);
 void priskv_crc_ctx_destroy(priskv_crc_ctx *ctx);
 int priskv_crc_ctx_device(const priskv_crc_ctx *ctx);
@@ -62,7 +64,10 @@ int priskv_crc32_blocks_dev(const priskv_crc_ctx *ctx, const void *d_base, uint6
 /* Device-resident per-value extents: d_out[i] = priskv_crc32(d_base +
  * d_offsets[i], d_lengths[i]) -- a value of valuelen bytes starting at
  * value_off (priskv_key, server/memory.h:50-51).  d_offsets / d_lengths /
- * d_out are device arrays of n entries.  Asynchronous on `stream`. */
+ * d_out are device arrays of n entries.  Asynchronous on `stream`.  With few
+ * extents (n <= 512) each is split into segments on the device, which needs a
+ * small scratch allocation ordered on `stream` (hipMallocAsync); -ENOMEM if
+ * that fails. */
 int priskv_crc32_ranges_dev(const priskv_crc_ctx *ctx, const void *d_base,
                             const uint64_t *d_offsets, const uint32_t *d_lengths, uint64_t n,
                             uint32_t *d_out, void *stream);
