@@ -393,6 +393,14 @@ int main(int argc, char **argv)
     all.push_back(CRC_VARIANT_W(32, 8, 2, 2, 1, 2, 31, 29));
     all.push_back(NIB_VARIANT_W(32, 8, 2, 2, 1, 2, 31, 29));
     all.push_back(S8_VARIANT_W(32, 8, 2, 2, 1, 2, 31, 29));
+    all.push_back(NIB_VARIANT_W(32, 8, 2, 0, 1, 2, 31, 29));
+    all.push_back(NIB_VARIANT_W(32, 8, 2, 3, 1, 2, 31, 29));
+    all.push_back(NIB_VARIANT_W(32, 8, 2, 16, 1, 2, 31, 29));
+    all.push_back(NIB_VARIANT_W(32, 8, 2, 18, 1, 2, 31, 29));
+    all.push_back(NIB_VARIANT_W(32, 8, 2, 19, 1, 2, 31, 29));
+    all.push_back(ROOF_VARIANT_W(32, 8, 2, 0, 1, 31, 29));
+    all.push_back(ROOF_VARIANT_W(32, 8, 2, 3, 1, 31, 29));
+    all.push_back(ROOF_VARIANT_W(32, 8, 2, 18, 1, 31, 29));
     all.push_back(TAIL_VARIANT(32, 8, 2, 2, 34, 31, 29, 8, 4));
     all.push_back(TAIL_VARIANT(32, 8, 2, 2, 34, 31, 29, 4, 8));
     all.push_back(TAIL_VARIANT(32, 8, 2, 2, 34, 31, 29, 16, 4));
