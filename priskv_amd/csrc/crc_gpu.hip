@@ -368,11 +368,14 @@ int launch_rows(const priskv_crc_ctx *ctx, const uint8_t *base, uint64_t nblocks
         return rc;
     int rc = launch_rows_plain(ctx, base, nblocks * S, bs / S, sub, s);
     if (!rc) {
-        ZCols z;
-        prv_shift_columns(z.c, bs / S);
-        const uint64_t want = (nblocks + 255) / 256;
-        const uint32_t grid = (uint32_t)(want < (uint64_t)ctx->num_cus * 4 ? want : (uint64_t)ctx->num_cus * 4);
-        hipLaunchKernelGGL(crc_combine_segments_kernel, dim3(grid), dim3(256), 0, s, sub, nblocks, S, z, out);
+        const uint32_t r = S > 64 ? S / 64 : 1; // segments per lane (S is a power of two)
+        SegCols z;
+        prv_shift_columns(z.c[0], bs / S);
+        for (int b = 0; b < 6; b++)
+            prv_shift_columns(z.c[1 + b], (uint64_t)(bs / S) * r << b);
+        const uint64_t want = (nblocks + 3) / 4; // one wave per block
+        const uint32_t grid = (uint32_t)(want < (uint64_t)ctx->num_cus * 8 ? want : (uint64_t)ctx->num_cus * 8);
+        hipLaunchKernelGGL(crc_combine_segments_kernel, dim3(grid), dim3(256), 0, s, sub, nblocks, S, r, z, out);
         rc = herr(hipGetLastError());
     }
     const int frc = herr(hipFreeAsync(sub, s));

@@ -249,7 +249,8 @@ def test_ranges_chunk_boundaries(torch_cuda, any_ctx):
 
 
 @pytest.mark.parametrize("bs,nb", [(1 << 20, 1), (1 << 20, 3), (1 << 20, 100), (2 << 20, 5), (4 << 20, 2),
-                                   (48 << 10, 7), (3 << 20, 1), (1025 << 10, 3), (96 << 10, 1000)])
+                                   (48 << 10, 7), (3 << 20, 1), (1025 << 10, 3), (96 << 10, 1000),
+                                   (64 << 20, 1), (48 << 20, 2), (3 << 24, 1)])
 def test_segmented_large_blocks(torch_cuda, ctx, bs, nb):
     """Batches of few large blocks are hashed as equal segments and combined
     with Z_seg (crc_combine_segments_kernel); results must not change."""

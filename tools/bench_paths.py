@@ -121,6 +121,26 @@ def few_values_case(ctx, ctx_noseg):
         del t
 
 
+def few_blocks_case(ctx, ctx_noseg):
+    """Few very large blocks (the rows path's segmentation + combine) against
+    the unsegmented rows kernel, same process."""
+    for count, bs in ((1, 256 << 20), (4, 64 << 20), (16, 16 << 20), (1024, 1 << 20)):
+        t = torch.empty(count * bs, dtype=torch.uint8, device="cuda")
+        ctx.fill_splitmix(t, SEED, 0)
+        res, outs = {}, {}
+        for name, c in (("segmented", ctx), ("unsegmented", ctx_noseg)):
+            out = torch.empty(count, dtype=torch.int32, device="cuda")
+            sec = timeit(lambda: c.blocks_dev(t, bs, out=out), 10)
+            res[name] = (round(sec * 1e6, 1), round(count * bs / sec / 2**30, 1))
+            outs[name] = as_u32(out)
+        ok = np.array_equal(outs["segmented"], outs["unsegmented"]) and \
+            outs["segmented"][0] == O.crc32(t[:bs].cpu().numpy())
+        emit(path="blocks_dev_few_large", blocks=count, block_size=bs, segmented_us=res["segmented"][0],
+             segmented_GiBs=res["segmented"][1], unsegmented_us=res["unsegmented"][0],
+             unsegmented_GiBs=res["unsegmented"][1], bit_exact=bool(ok))
+        del t
+
+
 def ranges_host_case(ctx, bs=4096, region=2 << 30, n=1 << 17):
     rng = np.random.default_rng(2)
     host = O.fill_splitmix(region, SEED, 0)
@@ -215,6 +235,7 @@ def main():
         ctx_noseg = CrcContext(0)
         del os.environ["PRISKV_CRC_SEGMENT"]
         few_values_case(ctx, ctx_noseg)
+        few_blocks_case(ctx, ctx_noseg)
         ctx_noseg.close()
     if "host" in which:
         ranges_host_case(ctx)
