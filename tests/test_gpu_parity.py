@@ -550,6 +550,45 @@ def test_concurrent_streams_and_threads(torch_cuda, ctx):
             assert np.array_equal(a, want[k][0]) and np.array_equal(b, want[k][1]) and np.array_equal(c, want[k][2])
 
 
+def test_hip_graph_capture_and_replay(torch_cuda, ctx):
+    """The *_dev calls are pure stream work (kernels, stream-ordered scratch):
+    they capture into a HIP graph and replay on new data with correct results --
+    the rows plan, the segmented rows path (few large blocks: scratch + combine)
+    and the segmented extents path (plan / segments / reduce)."""
+    torch = torch_cuda
+    n = 40 << 20
+    t = _region(torch, ctx, n, SEED ^ 0x6A, 2)
+    offs = np.array([5, 3 << 20, 20 << 20], dtype=np.uint64)
+    lens = np.array([(3 << 20) - 9, 17 << 20, 100], dtype=np.uint32)
+    d_o = torch.from_numpy(offs.astype(np.int64)).cuda()
+    d_l = torch.from_numpy(lens.view(np.int32)).cuda()
+    o1 = torch.empty(1000, dtype=torch.int32, device="cuda")
+    o2 = torch.empty(2, dtype=torch.int32, device="cuda")
+    o3 = torch.empty(3, dtype=torch.int32, device="cuda")
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):  # warm-up outside capture
+        ctx.blocks_dev(t, 4096, out=o1, nblocks=1000, stream=s)
+        ctx.blocks_dev(t, 16 << 20, out=o2, nblocks=2, stream=s)
+        ctx.ranges_dev(t, d_o, d_l, out=o3, stream=s)
+    torch.cuda.current_stream().wait_stream(s)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        st = torch.cuda.current_stream()
+        ctx.blocks_dev(t, 4096, out=o1, nblocks=1000, stream=st)
+        ctx.blocks_dev(t, 16 << 20, out=o2, nblocks=2, stream=st)
+        ctx.ranges_dev(t, d_o, d_l, out=o3, stream=st)
+    for seed in (11, 12):
+        ctx.fill_splitmix(t, seed, 0)
+        g.replay()
+        torch.cuda.synchronize()
+        host = t[:n].cpu().numpy()
+        assert np.array_equal(_u32(o1), O.crc32_blocks(host[: 4096 * 1000], 4096, nthreads=8))
+        assert np.array_equal(_u32(o2), O.crc32_blocks(host[: 32 << 20], 16 << 20, nthreads=8))
+        assert np.array_equal(_u32(o3), O.crc32_ranges(host, offs, lens))
+
+
 def test_bad_args_on_gpu(torch_cuda, ctx):
     from priskv_amd.crc import lib
     L = lib()
