@@ -647,6 +647,30 @@ int main(int argc, char **argv)
             for (int x = 0; x < 8; x++)
                 printf(" %.1f", xn[x] ? xe[x] / xn[x] : 0.0);
             printf("\n");
+            // within-workgroup (one CU) spread vs across workgroups
+            {
+                std::vector<double> wspread, wmax, wmin;
+                for (uint32_t b = 0; b < grid; b++) {
+                    double mx = 0, mn = 1e30;
+                    for (int k = 0; k < kWaves; k++) {
+                        mx = std::max(mx, en[b * kWaves + k]);
+                        mn = std::min(mn, en[b * kWaves + k]);
+                    }
+                    wspread.push_back(mx - mn);
+                    wmax.push_back(mx);
+                    wmin.push_back(mn);
+                }
+                std::sort(wspread.begin(), wspread.end());
+                std::sort(wmax.begin(), wmax.end());
+                std::sort(wmin.begin(), wmin.end());
+                double ms = 0;
+                for (double v : wspread)
+                    ms += v;
+                printf("  per-CU: end spread inside a workgroup mean %.1f p50 %.1f p90 %.1f us | workgroup "
+                       "last-wave end p0 %.1f p50 %.1f p100 %.1f | first-wave end p50 %.1f\n",
+                       ms / wspread.size(), pc(wspread, 0.5), pc(wspread, 0.9), pc(wmax, 0.0), pc(wmax, 0.5),
+                       pc(wmax, 1.0), pc(wmin, 0.5));
+            }
         }
     }
     return ok_all ? 0 : 1;
