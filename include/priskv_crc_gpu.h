@@ -65,9 +65,9 @@ int priskv_crc32_blocks_dev(const priskv_crc_ctx *ctx, const void *d_base, uint6
  * d_offsets[i], d_lengths[i]) -- a value of valuelen bytes starting at
  * value_off (priskv_key, server/memory.h:50-51).  d_offsets / d_lengths /
  * d_out are device arrays of n entries.  Asynchronous on `stream`.  With few
- * extents (n <= 512) each is split into segments on the device, which needs a
- * small scratch allocation ordered on `stream` (hipMallocAsync); -ENOMEM if
- * that fails. */
+ * extents (n <= 2048; PRISKV_CRC_SEG_MAX_EXTENTS) each is split into segments
+ * on the device, which needs a small scratch allocation ordered on `stream`
+ * (hipMallocAsync); -ENOMEM if that fails. */
 int priskv_crc32_ranges_dev(const priskv_crc_ctx *ctx, const void *d_base,
                             const uint64_t *d_offsets, const uint32_t *d_lengths, uint64_t n,
                             uint32_t *d_out, void *stream);

@@ -58,6 +58,7 @@ struct priskv_crc_ctx {
     int plan_wgs_per_cu[8];    // resident workgroups per CU of each rows-kernel plan
     uint32_t xcd_weights;      // rows-kernel split: (even << 16) | odd XCD weight, 0 = equal
     int segment;               // split few large blocks / extents into segments (PRISKV_CRC_SEGMENT=0: off)
+    uint64_t seg_max_extents;  // device-resident lengths: segment calls of at most this many extents
     uint32_t *d_lds_image[3];  // 64 KiB each: set B gap for G = 64, 32, 16
     uint32_t *d_fold;          // kFoldSets x 2048 words, set j for G = 1 << j
     uint32_t *d_nibrep[7];     // nibble fold tables for G = 1 << j (j >= 1), 8 x 16 x max(G, 32) words
@@ -309,8 +310,12 @@ int launch_rows_plain(const priskv_crc_ctx *ctx, const uint8_t *base, uint64_t n
 // (one constant length on the blocks path, host arrays on the host scrub),
 // segment when the batch is unbalanced and that length is at least
 // kSegMinLen.  Device-resident lengths are unknown, so the rule uses the
-// count: at most kSegMaxExtents extents (an eighth of the resident waves).
-constexpr uint64_t kSegMaxExtents = 512;
+// count: at most kSegMaxExtents extents, half the resident waves.  At 2048
+// PrisKV-shaped values that costs small values ~16 us (4 KiB blocks: 10 ->
+// 26 us) and saves 0.5-0.8 ms on MiB values (1 MiB blocks: 1219 -> 747 us;
+// profiles/r01/seg_limit.jsonl); KV-cache values are the large kind.
+// PRISKV_CRC_SEG_MAX_EXTENTS moves the threshold (0 = never for device lengths).
+constexpr uint64_t kSegMaxExtents = 2048;
 constexpr uint32_t kSegMinLen = 64u << 10;
 
 int launch_extents_seg(const priskv_crc_ctx *ctx, const uint8_t *base, uint64_t n, const uint64_t *offs,
@@ -323,9 +328,9 @@ int launch_extents_seg(const priskv_crc_ctx *ctx, const uint8_t *base, uint64_t 
         max_len = len_const;
     if (!ctx->segment || n == 0 || n > 64ull * kSegPlanPerLane)
         return 0;
-    if (max_len ? (max_len < kSegMinLen || balanced(n, waves)) : n > kSegMaxExtents)
+    if (max_len ? (max_len < kSegMinLen || balanced(n, waves)) : n > ctx->seg_max_extents)
         return 0;
-    uint32_t cap_log2 = 6;
+    uint32_t cap_log2 = 6; // >= 64 segments per extent allowed (16-64 KiB segments beat fewer, larger ones)
     while (cap_log2 < 10 && (n << cap_log2) < 2 * waves)
         cap_log2++;
     const size_t off_shift = ((n + 1) * 4 + 255) / 256 * 256;
@@ -514,6 +519,11 @@ int priskv_crc_ctx_create(int device, priskv_crc_ctx **out)
     {
         const char *e = getenv("PRISKV_CRC_SEGMENT");
         c->segment = !(e && !strcmp(e, "0"));
+        c->seg_max_extents = kSegMaxExtents;
+        if (const char *m = getenv("PRISKV_CRC_SEG_MAX_EXTENTS")) { // capped by the plan kernel's 2048
+            const unsigned long long v = strtoull(m, nullptr, 10);
+            c->seg_max_extents = v < 64ull * kSegPlanPerLane ? v : 64ull * kSegPlanPerLane;
+        }
     }
     for (int j = 0; j < kFoldSets; j++)
         prv_fold_columns(h_fold + j * 2048, 1u << j);

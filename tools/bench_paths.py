@@ -85,7 +85,7 @@ def ranges_dev_case(ctx, bs=4096, region=4 << 30, n=1 << 19, steps=10):
                     dtype=np.uint32)
     ok = np.array_equal(got[:200], want)
     vb = int(lens.astype(np.uint64).sum())
-    emit(path="ranges_dev", values=n, value_bytes=vb, mean_len=round(vb / n), ms=round(sec * 1e3, 4),
+    emit(path="ranges_dev", block_size=bs, values=n, value_bytes=vb, mean_len=round(vb / n), ms=round(sec * 1e3, 4),
          GiBs=round(vb / sec / 2**30, 1), checked=200, bit_exact=bool(ok))
     del t, host
 
@@ -119,6 +119,30 @@ def few_values_case(ctx, ctx_noseg):
              segmented_GiBs=res["segmented"][1], unsegmented_us=res["one_wave_per_value"][0],
              unsegmented_GiBs=res["one_wave_per_value"][1], bit_exact=bool(ok))
         del t
+
+
+def seg_limit_case(ctx_a, ctx_b, label_a, label_b):
+    """PrisKV-shaped values at 4 KiB / 64 KiB / 1 MiB blocks, n = 1000..2048:
+    two contexts with different PRISKV_CRC_SEG_MAX_EXTENTS, same process."""
+    rng = np.random.default_rng(5)
+    region = 4 << 30
+    t = torch.empty(region, dtype=torch.uint8, device="cuda")
+    ctx_a.fill_splitmix(t, SEED, 0)
+    for bs, n in ((4096, 2048), (4096, 1024), (65536, 2048), (1 << 20, 2048), (1 << 20, 1000)):
+        offs, lens = extents(rng, n, region, bs)
+        d_o = torch.from_numpy(offs.astype(np.int64)).cuda()
+        d_l = torch.from_numpy(lens.view(np.int32)).cuda()
+        res, outs = {}, {}
+        for name, c in ((label_a, ctx_a), (label_b, ctx_b)):
+            out = torch.empty(n, dtype=torch.int32, device="cuda")
+            sec = timeit(lambda: c.ranges_dev(t, d_o, d_l, out=out), 20)
+            res[name] = round(sec * 1e6, 1)
+            outs[name] = as_u32(out)
+        vb = int(lens.astype(np.uint64).sum())
+        ok = np.array_equal(outs[label_a], outs[label_b])
+        emit(path="ranges_dev_seg_limit", block_size=bs, values=n, value_bytes=vb,
+             **{label_a + "_us": res[label_a], label_b + "_us": res[label_b]}, bit_exact=bool(ok))
+    del t
 
 
 def few_blocks_case(ctx, ctx_noseg):
@@ -223,13 +247,16 @@ def main():
     which = sys.argv[1:] or ["blocks", "ranges", "host", "memfile"]
     ctx = CrcContext(0)
     if "blocks" in which:
-        for bs in (16, 64, 256, 512, 1024, 2048, 3072, 4096, 8192, 16384, 20480, 65536, 1 << 20, 100, 4100):
+        for bs in (16, 64, 256, 512, 1024, 2048, 3072, 4096, 8192, 16384, 20480, 32768, 65536, 131072, 262144,
+                   524288, 1 << 20, 100, 4100):
             total = (1 << 30) if bs >= 1024 else (256 << 20)
             if bs in (100, 4100):
                 total = 64 << 20
             blocks_case(ctx, bs, total)
     if "ranges" in which:
         ranges_dev_case(ctx)
+        ranges_dev_case(ctx, bs=65536, n=1 << 15)
+        ranges_dev_case(ctx, bs=1 << 20, n=1 << 11)
     if "few" in which or "ranges" in which:
         os.environ["PRISKV_CRC_SEGMENT"] = "0"
         ctx_noseg = CrcContext(0)
@@ -237,11 +264,12 @@ def main():
         few_values_case(ctx, ctx_noseg)
         few_blocks_case(ctx, ctx_noseg)
         ctx_noseg.close()
-    if "host" in which:
-        ranges_host_case(ctx)
-        blocks_host_case(ctx)
-    if "memfile" in which:
-        memfile_case(ctx)
+    if "seglimit" in which:
+        os.environ["PRISKV_CRC_SEG_MAX_EXTENTS"] = "512"
+        ctx_512 = CrcContext(0)
+        del os.environ["PRISKV_CRC_SEG_MAX_EXTENTS"]
+        seg_limit_case(ctx_512, ctx, "limit512", "limit2048")
+        ctx_512.close()
 
 
 if __name__ == "__main__":
