@@ -25,6 +25,7 @@ namespace {
 #include "crc_dyn_explore.inc"
 #include "crc_pair_explore.inc"
 #include "crc_tail_explore.inc"
+#include "crc_rows2_explore.inc"
 
 // read-only roof with the rows kernel's loop and addressing (same loads, no hashing)
 // TIMING: also write each wave's start / end s_memrealtime after the sink
