@@ -326,7 +326,7 @@ int launch_extents_seg(const priskv_crc_ctx *ctx, const uint8_t *base, uint64_t 
     *used = false;
     if (!offs)
         max_len = len_const;
-    if (!ctx->segment || n == 0 || n > 64ull * kSegPlanPerLane)
+    if (!ctx->segment || n == 0 || n > (uint64_t)kSegPlanThreads * kSegPlanPerThread)
         return 0;
     if (max_len ? (max_len < kSegMinLen || balanced(n, waves)) : n > ctx->seg_max_extents)
         return 0;
@@ -341,7 +341,7 @@ int launch_extents_seg(const priskv_crc_ctx *ctx, const uint8_t *base, uint64_t 
     uint32_t *prefix = reinterpret_cast<uint32_t *>(scr);
     uint8_t *shifts = scr + off_shift;
     uint32_t *sub = reinterpret_cast<uint32_t *>(scr + off_sub);
-    hipLaunchKernelGGL(crc_seg_plan_kernel, dim3(1), dim3(64), 0, s, offs ? lens : nullptr, len_const, n, cap_log2,
+    hipLaunchKernelGGL(crc_seg_plan_kernel, dim3(1), dim3(kSegPlanThreads), 0, s, offs ? lens : nullptr, len_const, n, cap_log2,
                        prefix, shifts);
     int rc = herr(hipGetLastError());
     if (!rc) {
@@ -520,9 +520,10 @@ int priskv_crc_ctx_create(int device, priskv_crc_ctx **out)
         const char *e = getenv("PRISKV_CRC_SEGMENT");
         c->segment = !(e && !strcmp(e, "0"));
         c->seg_max_extents = kSegMaxExtents;
-        if (const char *m = getenv("PRISKV_CRC_SEG_MAX_EXTENTS")) { // capped by the plan kernel's 2048
+        if (const char *m = getenv("PRISKV_CRC_SEG_MAX_EXTENTS")) { // capped by the plan kernel's 16384
             const unsigned long long v = strtoull(m, nullptr, 10);
-            c->seg_max_extents = v < 64ull * kSegPlanPerLane ? v : 64ull * kSegPlanPerLane;
+            const uint64_t cap = (uint64_t)kSegPlanThreads * kSegPlanPerThread;
+            c->seg_max_extents = v < cap ? v : cap;
         }
     }
     for (int j = 0; j < kFoldSets; j++)

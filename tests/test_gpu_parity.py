@@ -52,6 +52,40 @@ def ctx_noseg(torch_cuda):
     c.close()
 
 
+@pytest.fixture(scope="module")
+def ctx_seg16k(torch_cuda):
+    """Segmentation for device-length calls of up to 16384 extents
+    (PRISKV_CRC_SEG_MAX_EXTENTS, read at creation)."""
+    import os
+    from priskv_amd import CrcContext
+    os.environ["PRISKV_CRC_SEG_MAX_EXTENTS"] = "16384"
+    try:
+        c = CrcContext(0)
+    finally:
+        del os.environ["PRISKV_CRC_SEG_MAX_EXTENTS"]
+    yield c
+    c.close()
+
+
+def test_segmented_many_extents(torch_cuda, ctx_seg16k):
+    """Thousands of extents through the segmented path (1024-thread plan, 64-way
+    segment search): mixed lengths incl. empty and sub-16-B ones, ragged offsets."""
+    torch = torch_cuda
+    ctx = ctx_seg16k
+    n_bytes = 256 << 20
+    t = _region(torch, ctx, n_bytes, SEED ^ 0x99, 4)
+    rng = np.random.default_rng(31)
+    for k in (2049, 5000, 16384):
+        lens = rng.integers(0, 200000, k).astype(np.uint32)
+        lens[:8] = [0, 1, 15, 16, 17, 16384, 16385, 1 << 20]
+        offs = np.array([rng.integers(0, n_bytes - int(ln)) for ln in lens], dtype=np.uint64)
+        got = _u32(ctx.ranges_dev(t, torch.from_numpy(offs.astype(np.int64)).cuda(),
+                                  torch.from_numpy(lens.view(np.int32)).cuda()))
+        torch.cuda.synchronize()
+        want = O.crc32_ranges(t[:n_bytes].cpu().numpy(), offs, lens)
+        assert np.array_equal(got, want), (k, np.nonzero(got != want)[0][:8])
+
+
 @pytest.fixture(params=["segmented", "unsegmented"])
 def any_ctx(request, ctx, ctx_noseg):
     return ctx if request.param == "segmented" else ctx_noseg

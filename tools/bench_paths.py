@@ -128,7 +128,8 @@ def seg_limit_case(ctx_a, ctx_b, label_a, label_b):
     region = 4 << 30
     t = torch.empty(region, dtype=torch.uint8, device="cuda")
     ctx_a.fill_splitmix(t, SEED, 0)
-    for bs, n in ((4096, 2048), (4096, 1024), (65536, 2048), (1 << 20, 2048), (1 << 20, 1000)):
+    for bs, n in ((4096, 2048), (4096, 8192), (4096, 16384), (65536, 2048), (65536, 8192), (65536, 16384),
+                  (1 << 20, 1000), (1 << 20, 2048), (1 << 20, 4096), (1 << 20, 8192), (1 << 20, 16384)):
         offs, lens = extents(rng, n, region, bs)
         d_o = torch.from_numpy(offs.astype(np.int64)).cuda()
         d_l = torch.from_numpy(lens.view(np.int32)).cuda()
@@ -141,7 +142,8 @@ def seg_limit_case(ctx_a, ctx_b, label_a, label_b):
         vb = int(lens.astype(np.uint64).sum())
         ok = np.array_equal(outs[label_a], outs[label_b])
         emit(path="ranges_dev_seg_limit", block_size=bs, values=n, value_bytes=vb,
-             **{label_a + "_us": res[label_a], label_b + "_us": res[label_b]}, bit_exact=bool(ok))
+             **{label_a + "_us": res[label_a], label_b + "_us": res[label_b]},
+             best_TBs=round(vb / min(res.values()) / 1e6, 3), bit_exact=bool(ok))
     del t
 
 
@@ -267,9 +269,12 @@ def main():
     if "seglimit" in which:
         os.environ["PRISKV_CRC_SEG_MAX_EXTENTS"] = "512"
         ctx_512 = CrcContext(0)
+        os.environ["PRISKV_CRC_SEG_MAX_EXTENTS"] = "16384"
+        ctx_16k = CrcContext(0)
         del os.environ["PRISKV_CRC_SEG_MAX_EXTENTS"]
-        seg_limit_case(ctx_512, ctx, "limit512", "limit2048")
+        seg_limit_case(ctx_512, ctx_16k, "limit512", "limit16384")
         ctx_512.close()
+        ctx_16k.close()
 
 
 if __name__ == "__main__":
