@@ -56,7 +56,7 @@ struct priskv_crc_ctx {
     int num_cus;
     int max_wgs;               // resident workgroups of the sub-KiB kernel (2 per CU)
     int plan_wgs_per_cu[8];    // resident workgroups per CU of each rows-kernel plan
-    uint32_t xcd_weights;      // rows-kernel split: (even << 16) | odd XCD weight, 0 = equal
+    uint32_t plan_xw[8];       // rows-kernel split per plan: (even << 16) | odd XCD weight, 0 = equal
     int segment;               // split few large blocks / extents into segments (PRISKV_CRC_SEGMENT=0: off)
     uint64_t seg_max_extents;  // device-resident lengths: segment calls of at most this many extents
     uint32_t *d_lds_image[3];  // 64 KiB each: set B gap for G = 64, 32, 16
@@ -197,12 +197,17 @@ enum PlanId {
     PLAN_G64_CH1,
     NPLANS
 };
+static_assert(NPLANS <= 8, "priskv_crc_ctx per-plan arrays");
 struct Plan {
     int G, CH, opt, wg_per_cu;
+    uint32_t we, wo; // even:odd XCD weights of the static split
 };
-// opt = crc_rows_kernel OPT bits: 2 = pipelined fold, 32 = nibble-table fold
-constexpr Plan kPlans[NPLANS] = {{32, 8, 2 | 32, 1}, {64, 4, 32, 1}, {16, 4, 2 | 32, 2}, {16, 4, 0, 2},
-                                 {64, 4, 0, 1}, {64, 2, 0, 1}, {64, 1, 0, 1}};
+// opt = crc_rows_kernel OPT bits: 2 = pipelined fold, 32 = nibble-table fold.
+// Weights: swept per plan (profiles/r01/explore_*_xw*.log, bench_xw_ab_*.log);
+// 31:29 is best or within noise for every plan in bench.py's sustained loop.
+constexpr Plan kPlans[NPLANS] = {{32, 8, 2 | 32, 1, 31, 29},   {64, 4, 32, 1, 31, 29}, {16, 4, 2 | 32, 2, 31, 29},
+                                 {16, 4, 0, 2, 31, 29},      {64, 4, 0, 1, 31, 29},  {64, 2, 0, 1, 31, 29},
+                                 {64, 1, 0, 1, 31, 29}};
 
 int plan_for(uint32_t bs)
 {
@@ -256,7 +261,7 @@ int launch_plan(const priskv_crc_ctx *ctx, int p, const uint8_t *base, uint64_t 
         const uint32_t *img = ctx->d_lds_image[gi];
         const uint32_t *fold = (P.opt & 32) ? ctx->d_nibrep[log2u(P.G)] : ctx->d_fold + log2u(P.G) * 2048;
         // weights move whole groups: only worth it with many groups per wave
-        uint32_t xw = n >= 32ull * grid * kWaves ? ctx->xcd_weights : 0u;
+        uint32_t xw = n >= 32ull * grid * kWaves ? ctx->plan_xw[p] : 0u;
         void *args[] = {(void *)&b, (void *)&n, (void *)&bs, (void *)&img, (void *)&fold, (void *)&o, (void *)&xw};
         if (int rc = herr(hipLaunchKernel(plan_fn(p), dim3(grid), dim3(kThreads), args, 0, s)))
             return rc;
@@ -443,12 +448,12 @@ int launch_blocks(const priskv_crc_ctx *ctx, const uint8_t *base, uint64_t nbloc
 
 // XCD weights of the rows-kernel split: on a multi-XCD device
 // (workgroups dispatched round-robin over 8 XCDs) waves on odd XCDs finish
-// ~10 % later under an equal split on every MI355X measured, so even-XCD
-// waves take 31 parts to odd 29.  PRISKV_CRC_XCD_WEIGHTS="we:wo" overrides
-// ("1:1" = equal split).
-uint32_t xcd_weights(int num_cus)
+// later under an equal split on every MI355X measured, so even-XCD waves take
+// more parts (kPlans[p].we : wo).  PRISKV_CRC_XCD_WEIGHTS="we:wo" overrides
+// every plan ("1:1" = equal split).
+uint32_t xcd_weights(int num_cus, int p)
 {
-    uint32_t we = 31, wo = 29;
+    uint32_t we = kPlans[p].we, wo = kPlans[p].wo;
     if (num_cus < 64 || num_cus % 8) // one XCD (or a partition mode): nothing to balance
         we = wo = 1;
     if (const char *e = getenv("PRISKV_CRC_XCD_WEIGHTS")) {
@@ -515,7 +520,8 @@ int priskv_crc_ctx_create(int device, priskv_crc_ctx **out)
     if ((rc = herr(hipDeviceGetAttribute(&c->num_cus, hipDeviceAttributeMultiprocessorCount, device))))
         goto fail;
     c->max_wgs = 2 * c->num_cus;
-    c->xcd_weights = xcd_weights(c->num_cus);
+    for (int p = 0; p < NPLANS; p++)
+        c->plan_xw[p] = xcd_weights(c->num_cus, p);
     {
         const char *e = getenv("PRISKV_CRC_SEGMENT");
         c->segment = !(e && !strcmp(e, "0"));

@@ -394,6 +394,23 @@ int main(int argc, char **argv)
     all.push_back(CRC_VARIANT_W(32, 8, 2, 2, 1, 2, 31, 29));
     all.push_back(NIB_VARIANT_W(32, 8, 2, 2, 1, 2, 31, 29));
     all.push_back(S8_VARIANT_W(32, 8, 2, 2, 1, 2, 31, 29));
+    all.push_back(NIB_VARIANT_W(32, 8, 2, 2, 1, 2, 0, 0));
+    all.push_back(NIB_VARIANT_W(32, 8, 2, 2, 1, 2, 61, 59));
+    all.push_back(NIB_VARIANT_W(32, 8, 2, 2, 1, 2, 41, 39));
+    all.push_back(NIB_VARIANT_W(32, 8, 2, 2, 1, 2, 21, 19));
+    all.push_back(NIB_VARIANT_W(32, 8, 2, 2, 1, 2, 33, 27));
+    all.push_back(NIB_VARIANT_W(32, 8, 2, 2, 1, 2, 8, 7));
+    all.push_back(CRC_VARIANT_W(64, 4, 2, 2, 1, 0, 8, 7));
+    all.push_back(CRC_VARIANT_W(64, 4, 2, 2, 1, 0, 21, 19));
+    all.push_back(CRC_VARIANT_W(64, 4, 2, 2, 1, 0, 0, 0));
+    all.push_back(NIB_VARIANT_W(64, 4, 2, 2, 1, 0, 8, 7));
+    all.push_back(NIB_VARIANT_W(64, 4, 2, 2, 1, 0, 21, 19));
+    all.push_back(NIB_VARIANT_W(64, 4, 2, 2, 1, 0, 0, 0));
+    all.push_back(NIB_VARIANT_W(32, 8, 2, 2, 1, 2, 7, 6));
+    all.push_back(NIB_VARIANT_W(32, 8, 2, 2, 1, 2, 6, 5));
+    all.push_back(NIB_VARIANT_W(32, 8, 2, 2, 1, 2, 5, 4));
+    all.push_back(NIB_VARIANT_W(32, 8, 2, 2, 1, 2, 9, 7));
+    all.push_back(NIB_VARIANT_W(32, 8, 2, 2, 1, 2, 4, 3));
     all.push_back(NIB_VARIANT_W(32, 8, 2, 0, 1, 2, 31, 29));
     all.push_back(NIB_VARIANT_W(32, 8, 2, 3, 1, 2, 31, 29));
     all.push_back(NIB_VARIANT_W(32, 8, 2, 16, 1, 2, 31, 29));
