@@ -254,7 +254,12 @@ def ctx_path(bs, region):
         fold = ",pipelined-fold" if pipe else ""
         if bs in (1024, 4096, 8192):
             fold += ",nibble-table-fold"
-        return f"crc_rows_kernel<G={g},CH={ch},NBUF=2,nt{fold}{split}>"
+        # progress-priority mode of the plan (kPlans in crc_gpu.hip)
+        mode = 3 if bs == 4096 or (g == 64 and ch == 4 and bs >= 256 << 10) else (1 if ch == 4 or g == 16 else 0)
+        if os.environ.get("PRISKV_CRC_PRIO") == "0":
+            mode = 0
+        prio = f",progress-priority {mode}" if mode else ""
+        return f"crc_rows_kernel<G={g},CH={ch},NBUF=2,nt{fold}{split}{prio}>"
     return f"crc_{p}_kernel"
 
 

@@ -58,6 +58,7 @@ struct priskv_crc_ctx {
     int plan_wgs_per_cu[8];    // resident workgroups per CU of each rows-kernel plan
     uint32_t plan_xw[8];       // rows-kernel split per plan: (even << 16) | odd XCD weight, 0 = equal
     int segment;               // split few large blocks / extents into segments (PRISKV_CRC_SEGMENT=0: off)
+    int prio;                  // rows kernel progress priority (PRISKV_CRC_PRIO=0: off)
     uint64_t seg_max_extents;  // device-resident lengths: segment calls of at most this many extents
     uint32_t *d_lds_image[3];  // 64 KiB each: set B gap for G = 64, 32, 16
     uint32_t *d_fold;          // kFoldSets x 2048 words, set j for G = 1 << j
@@ -193,6 +194,7 @@ enum PlanId {
     PLAN_G16_CH4_PIPE, // 1 KiB (same two folds)
     PLAN_G16_CH4,      // other multiples of 1 KiB up to 16 KiB
     PLAN_G64_CH4,      // 12 KiB and up (multiples of 4 KiB)
+    PLAN_G64_CH4_BIG,  // 256 KiB and up (multiples of 4 KiB)
     PLAN_G64_CH2,
     PLAN_G64_CH1,
     NPLANS
@@ -202,12 +204,15 @@ struct Plan {
     int G, CH, opt, wg_per_cu;
     uint32_t we, wo; // even:odd XCD weights of the static split
 };
-// opt = crc_rows_kernel OPT bits: 2 = pipelined fold, 32 = nibble-table fold.
-// Weights: swept per plan (profiles/r01/explore_*_xw*.log, bench_xw_ab_*.log);
+// opt = crc_rows_kernel OPT bits: 2 = pipelined fold, 32 = nibble-table fold,
+// (m << 8) = progress-priority mode m (profiles/r01/explore_*_prio*.log).
+// Weights: swept per plan (profiles/r01/explore_*_xw*.log, bench_xw_ab.jsonl);
 // 31:29 is best or within noise for every plan in bench.py's sustained loop.
-constexpr Plan kPlans[NPLANS] = {{32, 8, 2 | 32, 1, 31, 29},   {64, 4, 32, 1, 31, 29}, {16, 4, 2 | 32, 2, 31, 29},
-                                 {16, 4, 0, 2, 31, 29},      {64, 4, 0, 1, 31, 29},  {64, 2, 0, 1, 31, 29},
-                                 {64, 1, 0, 1, 31, 29}};
+constexpr int kPrio1 = 1 << 8, kPrio3 = 3 << 8;
+constexpr Plan kPlans[NPLANS] = {
+    {32, 8, 2 | 32 | kPrio3, 1, 31, 29}, {64, 4, 32 | kPrio1, 1, 31, 29}, {16, 4, 2 | 32 | kPrio1, 2, 31, 29},
+    {16, 4, kPrio1, 2, 31, 29},          {64, 4, kPrio1, 1, 31, 29},      {64, 4, kPrio3, 1, 31, 29},
+    {64, 2, 0, 1, 31, 29},               {64, 1, 0, 1, 31, 29}};
 
 int plan_for(uint32_t bs)
 {
@@ -220,7 +225,9 @@ int plan_for(uint32_t bs)
     if (bs <= (16u << 10) && bs % 4096 != 0)
         return PLAN_G16_CH4;
     const uint32_t R = bs / PRV_ROW_BYTES;
-    return R % 4 == 0 ? PLAN_G64_CH4 : (R % 2 == 0 ? PLAN_G64_CH2 : PLAN_G64_CH1);
+    if (R % 4 == 0)
+        return bs >= (256u << 10) ? PLAN_G64_CH4_BIG : PLAN_G64_CH4;
+    return R % 2 == 0 ? PLAN_G64_CH2 : PLAN_G64_CH1;
 }
 
 template <int G, int CH, int OPT>
@@ -229,16 +236,25 @@ const void *plan_kernel()
     return reinterpret_cast<const void *>(&crc_rows_kernel<G, CH, kNbuf, kAux, OPT>);
 }
 
-const void *plan_fn(int p)
+// prio = false: the plan's kernel without progress priority (PRISKV_CRC_PRIO=0)
+template <int P>
+const void *plan_kernel_p(bool prio)
+{
+    constexpr Plan Q = kPlans[P];
+    return prio ? plan_kernel<Q.G, Q.CH, Q.opt>() : plan_kernel<Q.G, Q.CH, (Q.opt & ~(3 << 8))>();
+}
+
+const void *plan_fn(int p, bool prio)
 {
     switch (p) {
-    case PLAN_G32_CH8_PIPE: return plan_kernel<32, 8, 2 | 32>();
-    case PLAN_G64_CH4_NIB: return plan_kernel<64, 4, 32>();
-    case PLAN_G16_CH4_PIPE: return plan_kernel<16, 4, 2 | 32>();
-    case PLAN_G16_CH4: return plan_kernel<16, 4, 0>();
-    case PLAN_G64_CH4: return plan_kernel<64, 4, 0>();
-    case PLAN_G64_CH2: return plan_kernel<64, 2, 0>();
-    default: return plan_kernel<64, 1, 0>();
+    case PLAN_G32_CH8_PIPE: return plan_kernel_p<PLAN_G32_CH8_PIPE>(prio);
+    case PLAN_G64_CH4_NIB: return plan_kernel_p<PLAN_G64_CH4_NIB>(prio);
+    case PLAN_G16_CH4_PIPE: return plan_kernel_p<PLAN_G16_CH4_PIPE>(prio);
+    case PLAN_G16_CH4: return plan_kernel_p<PLAN_G16_CH4>(prio);
+    case PLAN_G64_CH4: return plan_kernel_p<PLAN_G64_CH4>(prio);
+    case PLAN_G64_CH4_BIG: return plan_kernel_p<PLAN_G64_CH4_BIG>(prio);
+    case PLAN_G64_CH2: return plan_kernel_p<PLAN_G64_CH2>(prio);
+    default: return plan_kernel_p<PLAN_G64_CH1>(prio);
     }
 }
 
@@ -263,7 +279,7 @@ int launch_plan(const priskv_crc_ctx *ctx, int p, const uint8_t *base, uint64_t 
         // weights move whole groups: only worth it with many groups per wave
         uint32_t xw = n >= 32ull * grid * kWaves ? ctx->plan_xw[p] : 0u;
         void *args[] = {(void *)&b, (void *)&n, (void *)&bs, (void *)&img, (void *)&fold, (void *)&o, (void *)&xw};
-        if (int rc = herr(hipLaunchKernel(plan_fn(p), dim3(grid), dim3(kThreads), args, 0, s)))
+        if (int rc = herr(hipLaunchKernel(plan_fn(p, ctx->prio), dim3(grid), dim3(kThreads), args, 0, s)))
             return rc;
         done += n;
     }
@@ -472,7 +488,7 @@ int rows_occupancy(priskv_crc_ctx *c)
 {
     for (int p = 0; p < NPLANS; p++) {
         int n = 0;
-        hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, plan_fn(p), kThreads, 0);
+        hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, plan_fn(p, c->prio), kThreads, 0);
         if (e != hipSuccess)
             return herr(e);
         c->plan_wgs_per_cu[p] = n < 1 ? 1 : (n < kPlans[p].wg_per_cu ? n : kPlans[p].wg_per_cu);
@@ -525,6 +541,8 @@ int priskv_crc_ctx_create(int device, priskv_crc_ctx **out)
     {
         const char *e = getenv("PRISKV_CRC_SEGMENT");
         c->segment = !(e && !strcmp(e, "0"));
+        const char *pe = getenv("PRISKV_CRC_PRIO");
+        c->prio = !(pe && !strcmp(pe, "0"));
         c->seg_max_extents = kSegMaxExtents;
         if (const char *m = getenv("PRISKV_CRC_SEG_MAX_EXTENTS")) { // capped by the plan kernel's 16384
             const unsigned long long v = strtoull(m, nullptr, 10);

@@ -53,6 +53,39 @@ def ctx_noseg(torch_cuda):
 
 
 @pytest.fixture(scope="module")
+def ctx_noprio(torch_cuda):
+    """A context with the rows kernel's progress priority off
+    (PRISKV_CRC_PRIO=0, read at creation)."""
+    import os
+    from priskv_amd import CrcContext
+    old = os.environ.get("PRISKV_CRC_PRIO")
+    os.environ["PRISKV_CRC_PRIO"] = "0"
+    try:
+        c = CrcContext(0)
+    finally:
+        if old is None:
+            del os.environ["PRISKV_CRC_PRIO"]
+        else:
+            os.environ["PRISKV_CRC_PRIO"] = old
+    yield c
+    c.close()
+
+
+@pytest.mark.parametrize("bs", [1024, 3072, 4096, 8192, 65536, 131072, 262144, 1 << 20])
+def test_progress_priority_on_and_off(torch_cuda, ctx, ctx_noprio, bs):
+    """Every rows plan with and without its progress-priority mode: the same
+    CRCs as the oracle (priority only reorders instruction issue)."""
+    torch = torch_cuda
+    nb = max(1, (48 << 20) // bs) + 3
+    t = _region(torch, ctx, bs * nb, SEED ^ (bs * 7), nb)
+    want = O.crc32_blocks(t[: bs * nb].cpu().numpy(), bs, nthreads=8)
+    for c in (ctx, ctx_noprio):
+        got = _u32(c.blocks_dev(t, bs, nblocks=nb))
+        torch.cuda.synchronize()
+        assert np.array_equal(got, want), (bs, nb, np.nonzero(got != want)[0][:8])
+
+
+@pytest.fixture(scope="module")
 def ctx_seg16k(torch_cuda):
     """Segmentation for device-length calls of up to 16384 extents
     (PRISKV_CRC_SEG_MAX_EXTENTS, read at creation)."""
@@ -137,10 +170,10 @@ def test_golden_ranges_on_gpu(torch_cuda, ctx, golden):
 # (priskv_amd/csrc/crc_gpu.hip plan_for):
 #   G32/CH8 pipelined nibble fold (4K), G16/CH4 pipelined nibble fold (1K),
 #   G64/CH4 nibble fold (8K), G16/CH4 (2K, 3K, 5K, 6K),
-#   G64/CH4 (12K, 16K, 20K, 64K, 1M), G64/CH2 (18K), G64/CH1 (17K, 33K),
+#   G64/CH4 (12K, 16K, 20K, 64K, 128K; 256K and 1M with priority mode 3), G64/CH2 (18K), G64/CH1 (17K, 33K),
 #   sub-KiB (16..512), extents (>= 1 KiB not a multiple of 1 KiB), generic (smaller odd sizes)
 BLOCK_SIZES = [1024, 2048, 3072, 4096, 5120, 6144, 8192, 12288, 16384, 17408, 18432, 20480, 33792,
-               65536, 1 << 20, 16, 32, 64, 128, 256, 512, 1, 3, 100, 1000, 4097, 4100, 48, 1025, 1040,
+               65536, 131072, 262144, 1 << 20, 16, 32, 64, 128, 256, 512, 1, 3, 100, 1000, 4097, 4100, 48, 1025, 1040,
                65537, 70000]
 NBLOCKS = [1, 2, 7, 63, 64, 65, 129, 1000, 4099]
 

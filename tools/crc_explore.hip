@@ -400,6 +400,28 @@ int main(int argc, char **argv)
     all.push_back(NIB_VARIANT_W(32, 8, 2, 2, 1, 2, 21, 19));
     all.push_back(NIB_VARIANT_W(32, 8, 2, 2, 1, 2, 33, 27));
     all.push_back(NIB_VARIANT_W(32, 8, 2, 2, 1, 2, 8, 7));
+    all.push_back(NIB_VARIANT_W(32, 8, 2, 2, 1, 2 | 256, 31, 29));
+    all.push_back(NIB_VARIANT_W(32, 8, 2, 2, 1, 2 | 512, 31, 29));
+    all.push_back(NIB_VARIANT_W(32, 8, 2, 2, 1, 2 | 768, 31, 29));
+    all.push_back(NIB_VARIANT_W(32, 8, 2, 2, 1, 2 | 256, 0, 0));
+    all.push_back(NIB_VARIANT_W(32, 8, 2, 2, 1, 2 | 256, 8, 7));
+    all.push_back(NIB_VARIANT_W(32, 8, 2, 2, 1, 2 | 8 | 256, 31, 29));
+    all.push_back(CRC_VARIANT_W(64, 4, 2, 2, 1, 256, 31, 29));
+    all.push_back(CRC_VARIANT_W(64, 4, 2, 2, 1, 512, 31, 29));
+    all.push_back(CRC_VARIANT_W(64, 4, 2, 2, 1, 768, 31, 29));
+    all.push_back(NIB_VARIANT_W(64, 4, 2, 2, 1, 256, 31, 29));
+    all.push_back(NIB_VARIANT_W(64, 4, 2, 2, 1, 512, 31, 29));
+    all.push_back(NIB_VARIANT_W(64, 4, 2, 2, 1, 768, 31, 29));
+    all.push_back(NIB_VARIANT_W(32, 8, 2, 2, 1, 2 | 768, 8, 7));
+    all.push_back(NIB_VARIANT_W(16, 4, 2, 2, 2, 2 | 256, 31, 29));
+    all.push_back(NIB_VARIANT_W(16, 4, 2, 2, 2, 2 | 512, 31, 29));
+    all.push_back(NIB_VARIANT_W(16, 4, 2, 2, 2, 2 | 768, 31, 29));
+    all.push_back(CRC_VARIANT_W(16, 4, 2, 2, 2, 0, 31, 29));
+    all.push_back(CRC_VARIANT_W(16, 4, 2, 2, 2, 256, 31, 29));
+    all.push_back(CRC_VARIANT_W(16, 4, 2, 2, 2, 768, 31, 29));
+    all.push_back(CRC_VARIANT_W(64, 2, 2, 2, 1, 0, 31, 29));
+    all.push_back(CRC_VARIANT_W(64, 2, 2, 2, 1, 256, 31, 29));
+    all.push_back(CRC_VARIANT_W(64, 2, 2, 2, 1, 768, 31, 29));
     all.push_back(CRC_VARIANT_W(64, 4, 2, 2, 1, 0, 8, 7));
     all.push_back(CRC_VARIANT_W(64, 4, 2, 2, 1, 0, 21, 19));
     all.push_back(CRC_VARIANT_W(64, 4, 2, 2, 1, 0, 0, 0));
