@@ -153,7 +153,47 @@ int launch_generic(const priskv_crc_ctx *ctx, const uint8_t *base, uint64_t n, u
 constexpr int kNbuf = 2;  // register pipeline depth (chunks)
 constexpr int kAux = 2;   // cache policy of the streaming loads: nt
 constexpr int kExtRows = 2; // rows per chunk of the extents kernel (tools/ranges_explore)
-constexpr int kExtOpt = 3;  // extents kernel: nibble fold + row apply (bit 0), masks only where needed (bit 1)
+// extents kernel: nibble fold + row apply (bit 0), masks only where needed
+// (bit 1).  Two shapes (profiles/r01/prio/): two 8-wave workgroups per CU
+// (kExtOpt), and for calls with many extents per wave one 16-wave workgroup
+// per CU with progress-priority mode 3 (kExtOptMany: bits 8-9 and 10; the
+// progress slots do not fit beside two 80 KiB table sets in 160 KiB of LDS).
+// Many small values gain 5-7 %; a few large extents per wave lose 2-4 % in
+// the 16-wave shape, so they keep the first.
+constexpr int kExtOpt = 3;
+constexpr int kExtOptMany = 3 | (3 << 8) | 1024;
+constexpr uint64_t kExtManyPerWave = 32; // extents per resident wave for kExtOptMany
+constexpr int kExtWaves = kWaves;         // kExtOpt's shape: waves per workgroup ...
+constexpr int kExtWgPerCu = 2;            // ... and workgroups per CU (the same 16 waves per CU)
+static_assert(ext_waves(kExtOpt) == kExtWaves && ext_waves(kExtOptMany) == kExtWaves * kExtWgPerCu,
+              "both extents shapes hold 16 waves per CU");
+
+// many: the 16-wave shape (unless PRISKV_CRC_PRIO=0); seg: segmented items
+int launch_ext_kernel(const priskv_crc_ctx *ctx, bool seg, bool many, hipStream_t s, const uint8_t *abase,
+                      uint64_t n, const uint64_t *offs, const uint32_t *lens, uint64_t shift, uint64_t stride,
+                      uint32_t len_const, uint32_t *out, const uint32_t *prefix, const uint8_t *shifts,
+                      const uint32_t *zpow, uint32_t *sub)
+{
+    const uint32_t *img = ctx->d_lds_image[0], *nib = ctx->d_nib16, *rs = ctx->d_rowshift;
+    void *args[] = {(void *)&abase, (void *)&n,   (void *)&offs, (void *)&lens,   (void *)&shift,
+                    (void *)&stride, (void *)&len_const, (void *)&img, (void *)&nib, (void *)&rs,
+                    (void *)&out,   (void *)&prefix, (void *)&shifts, (void *)&zpow, (void *)&sub};
+    many = many && ctx->prio;
+    const int waves = many ? kExtWaves * kExtWgPerCu : kExtWaves;
+    const uint64_t cap = (uint64_t)ctx->num_cus * (many ? 1 : kExtWgPerCu);
+    // segmented: the grid covers every resident wave (the kernel reads the
+    // segment count on the device); else one wave per extent up to that
+    const uint64_t want = seg ? cap : (n + waves - 1) / waves;
+    const uint32_t grid = (uint32_t)(want < cap ? want : cap);
+    const void *fn;
+    if (seg)
+        fn = reinterpret_cast<const void *>(&crc_ranges_kernel<kExtRows, kNbuf, kAux, kExtOpt | 4>);
+    else if (many)
+        fn = reinterpret_cast<const void *>(&crc_ranges_kernel<kExtRows, kNbuf, kAux, kExtOptMany>);
+    else
+        fn = reinterpret_cast<const void *>(&crc_ranges_kernel<kExtRows, kNbuf, kAux, kExtOpt>);
+    return herr(hipLaunchKernel(fn, dim3(grid ? grid : 1), dim3(64 * waves), args, 0, s));
+}
 
 constexpr int kZpowRows = 48;
 
@@ -174,13 +214,9 @@ int launch_extents(const priskv_crc_ctx *ctx, const uint8_t *base, uint64_t n, c
         return 0;
     const uint64_t shift = (uintptr_t)base & 15;
     const uint8_t *abase = base - shift;
-    const uint64_t want = (n + kWaves - 1) / kWaves;
-    const uint64_t cap = (uint64_t)ctx->num_cus * 2;
-    const uint32_t grid = (uint32_t)(want < cap ? want : cap);
-    hipLaunchKernelGGL((crc_ranges_kernel<kExtRows, kNbuf, kAux, kExtOpt>), dim3(grid), dim3(kThreads), 0, s, abase,
-                       n, offs, lens, shift, stride, len_const, ctx->d_lds_image[0], ctx->d_nib16, ctx->d_rowshift,
-                       out, nullptr, nullptr, nullptr, nullptr);
-    return herr(hipGetLastError());
+    const bool many = n >= kExtManyPerWave * (uint64_t)ctx->num_cus * kExtWgPerCu * kExtWaves;
+    return launch_ext_kernel(ctx, false, many, s, abase, n, offs, lens, shift, stride, len_const, out, nullptr,
+                             nullptr, nullptr, nullptr);
 }
 
 // ---- rows kernel plans --------------------------------------------------------
@@ -343,7 +379,7 @@ int launch_extents_seg(const priskv_crc_ctx *ctx, const uint8_t *base, uint64_t 
                        const uint32_t *lens, uint64_t stride, uint32_t len_const, uint32_t *out, hipStream_t s,
                        uint64_t max_len, bool *used)
 {
-    const uint64_t waves = (uint64_t)ctx->num_cus * 2 * kWaves;
+    const uint64_t waves = (uint64_t)ctx->num_cus * kExtWgPerCu * kExtWaves;
     *used = false;
     if (!offs)
         max_len = len_const;
@@ -367,10 +403,8 @@ int launch_extents_seg(const priskv_crc_ctx *ctx, const uint8_t *base, uint64_t 
     int rc = herr(hipGetLastError());
     if (!rc) {
         const uint64_t sh = (uintptr_t)base & 15;
-        hipLaunchKernelGGL((crc_ranges_kernel<kExtRows, kNbuf, kAux, kExtOpt | 4>), dim3(ctx->num_cus * 2),
-                           dim3(kThreads), 0, s, base - sh, n, offs, lens, sh, stride, len_const, ctx->d_lds_image[0],
-                           ctx->d_nib16, ctx->d_rowshift, out, prefix, shifts, ctx->d_zpow, sub);
-        rc = herr(hipGetLastError());
+        rc = launch_ext_kernel(ctx, true, false, s, base - sh, n, offs, lens, sh, stride, len_const, out, prefix, shifts,
+                               ctx->d_zpow, sub);
     }
     if (!rc) {
         const uint32_t grid = (uint32_t)((n + 3) / 4);

@@ -119,9 +119,11 @@ def test_segmented_many_extents(torch_cuda, ctx_seg16k):
         assert np.array_equal(got, want), (k, np.nonzero(got != want)[0][:8])
 
 
-@pytest.fixture(params=["segmented", "unsegmented"])
-def any_ctx(request, ctx, ctx_noseg):
-    return ctx if request.param == "segmented" else ctx_noseg
+@pytest.fixture(params=["segmented", "unsegmented", "no-priority"])
+def any_ctx(request, ctx, ctx_noseg, ctx_noprio):
+    """The default context, one with segmentation off, and one with the
+    progress priority off (rows and extents kernels)."""
+    return {"segmented": ctx, "unsegmented": ctx_noseg, "no-priority": ctx_noprio}[request.param]
 
 
 def _region(torch, ctx, nbytes, seed=SEED, word_offset=0, pad=0):
@@ -473,6 +475,27 @@ def test_ranges_beyond_2GiB_and_many_per_wave(torch_cuda, ctx):
         o, ln = int(offs[i]), int(lens[i])
         assert got[i] == O.crc32(t[o:o + ln].cpu().numpy()), (i, o, ln)
     del t
+
+
+def test_ranges_many_per_wave_shapes(torch_cuda, any_ctx):
+    """Enough extents (>= 32 per resident wave) for the extents kernel's
+    16-wave progress-priority shape, with ragged offsets and lengths 0-9000 B,
+    against the oracle on every extent; the no-priority context runs the same
+    call in two 8-wave workgroups per CU."""
+    torch = torch_cuda
+    ctx = any_ctx
+    n = 96 << 20
+    t = _region(torch, ctx, n, SEED, 21)
+    rng = np.random.default_rng(22)
+    k = 200_000
+    lens = rng.integers(0, 9000, k).astype(np.uint32)
+    lens[:6] = [0, 1, 15, 16, 1024, 8999]
+    offs = rng.integers(0, n - 9000, k).astype(np.uint64)
+    out = ctx.ranges_dev(t, torch.from_numpy(offs.astype(np.int64)).cuda(), torch.from_numpy(lens.view(np.int32)).cuda())
+    torch.cuda.synchronize()
+    want = O.crc32_ranges(t[:n].cpu().numpy(), offs, lens)
+    got = _u32(out)
+    assert np.array_equal(got, want), np.nonzero(got != want)[0][:8]
 
 
 @pytest.mark.parametrize("register", [False, True])

@@ -73,6 +73,16 @@ static uint32_t *g_nib16 = nullptr, *g_rowshift = nullptr;
                                    ((OPT) & 1) ? g_rowshift : un, out, nullptr, nullptr, nullptr, nullptr);                         \
             }, false}
 
+// one 16-wave workgroup per CU (OPT bit 10)
+#define RVO16(CH, NB, AUX, OPT)                                                                                \
+    Variant{"ext CH" #CH " NBUF" #NB " AUX" #AUX " 16 waves opt" #OPT, 1,                                       \
+            [](dim3 g, const uint8_t *b, uint64_t n, const uint64_t *o, const uint32_t *l, uint64_t stride,       \
+               uint32_t lc, const uint32_t *img, const uint32_t *fold, const uint32_t *un, uint32_t *out) {       \
+                hipLaunchKernelGGL((crc_ranges_kernel<CH, NB, AUX, (OPT) | 1024>), g, dim3(1024), 0, 0, b, n, o, l, \
+                                   0ull, stride, lc, img, ((OPT) & 1) ? g_nib16 : fold,                           \
+                                   ((OPT) & 1) ? g_rowshift : un, out, nullptr, nullptr, nullptr, nullptr);       \
+            }, false}
+
 struct Set {
     const char *name;
     uint64_t n, stride;
@@ -171,8 +181,11 @@ int main(int argc, char **argv)
         sets.push_back(w);
     }
 
-    std::vector<Variant> V = {RV(2, 2, 2, 2),         RVO(2, 2, 2, 2, 1), RVO(2, 2, 2, 2, 2), RVO(2, 2, 2, 2, 3),
-                              RVO(1, 4, 2, 2, 3),     RVO(2, 3, 2, 2, 3), RVO(4, 2, 2, 2, 3)};
+    std::vector<Variant> V = {RVO(2, 2, 2, 2, 3),         RVO16(2, 2, 2, 3),       RVO16(2, 2, 2, 3 | 256),
+                              RVO16(2, 2, 2, 3 | 512),    RVO16(2, 2, 2, 3 | 768)};
+    if (getenv("RANGES_ALL")) // the earlier CH / NBUF / fold sweep
+        V = {RV(2, 2, 2, 2),     RVO(2, 2, 2, 2, 1), RVO(2, 2, 2, 2, 2), RVO(2, 2, 2, 2, 3),
+             RVO(1, 4, 2, 2, 3), RVO(2, 3, 2, 2, 3), RVO(4, 2, 2, 2, 3)};
     uint64_t nmax = 0;
     for (auto &s : sets)
         nmax = std::max(nmax, s.n);
