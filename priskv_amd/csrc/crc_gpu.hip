@@ -459,6 +459,31 @@ int launch_rows_plain(const priskv_crc_ctx *ctx, const uint8_t *base, uint64_t n
     return launch_plan(ctx, pt, base + head * (uint64_t)bs, nblocks - head, bs, out + head, s);
 }
 
+// sub-KiB kernel for G = 1 << gl: bit-matrix fold at G = 1; for G >= 2 the
+// nibble fold, with prio in one 16-wave workgroup per CU and progress-priority
+// mode 1 (+0.2-2.6 % at 32-512 B, profiles/r01/prio/small_*.log), else in two
+// 8-wave workgroups per CU (PRISKV_CRC_PRIO=0)
+constexpr int kSmallOptPrio = 1 | (1 << 8) | 1024;
+
+template <int G>
+const void *small_fn_g(bool prio)
+{
+    return prio ? reinterpret_cast<const void *>(&crc_small_kernel<G, kSmallOptPrio>)
+                : reinterpret_cast<const void *>(&crc_small_kernel<G, 1>);
+}
+
+const void *small_fn(int gl, bool prio)
+{
+    switch (gl) {
+    case 0: return reinterpret_cast<const void *>(&crc_small_kernel<1, 0>);
+    case 1: return small_fn_g<2>(prio);
+    case 2: return small_fn_g<4>(prio);
+    case 3: return small_fn_g<8>(prio);
+    case 4: return small_fn_g<16>(prio);
+    default: return small_fn_g<32>(prio);
+    }
+}
+
 int launch_blocks(const priskv_crc_ctx *ctx, const uint8_t *base, uint64_t nblocks, uint32_t bs,
                   uint32_t *out, hipStream_t s)
 {
@@ -470,19 +495,17 @@ int launch_blocks(const priskv_crc_ctx *ctx, const uint8_t *base, uint64_t nbloc
         const uint64_t per = 1024 / bs; // blocks per row
         const uint64_t nrows = nblocks / per;
         if (nrows) {
-            uint64_t want = (nrows + 4 * kWaves - 1) / (4 * kWaves);
-            uint32_t grid = (uint32_t)(want < (uint64_t)ctx->max_wgs ? want : (uint64_t)ctx->max_wgs);
             // G >= 2: nibble-table fold (replicated 32-wide tables)
             const uint32_t *fold = gl ? ctx->d_nibrep[gl] : ctx->d_fold;
             const uint32_t *img = ctx->d_lds_image[0];
-            switch (gl) {
-            case 0: hipLaunchKernelGGL((crc_small_kernel<1, 0>), dim3(grid), dim3(kThreads), 0, s, base, nrows, img, fold, out); break;
-            case 1: hipLaunchKernelGGL((crc_small_kernel<2, 1>), dim3(grid), dim3(kThreads), 0, s, base, nrows, img, fold, out); break;
-            case 2: hipLaunchKernelGGL((crc_small_kernel<4, 1>), dim3(grid), dim3(kThreads), 0, s, base, nrows, img, fold, out); break;
-            case 3: hipLaunchKernelGGL((crc_small_kernel<8, 1>), dim3(grid), dim3(kThreads), 0, s, base, nrows, img, fold, out); break;
-            case 4: hipLaunchKernelGGL((crc_small_kernel<16, 1>), dim3(grid), dim3(kThreads), 0, s, base, nrows, img, fold, out); break;
-            default: hipLaunchKernelGGL((crc_small_kernel<32, 1>), dim3(grid), dim3(kThreads), 0, s, base, nrows, img, fold, out); break;
-            }
+            const bool prio = gl && ctx->prio;
+            const int waves = prio ? 2 * kWaves : kWaves;
+            const uint64_t cap = prio ? (uint64_t)ctx->num_cus : (uint64_t)ctx->max_wgs;
+            const uint64_t want = (nrows + 4 * waves - 1) / (4 * waves);
+            const uint32_t grid = (uint32_t)(want < cap ? want : cap);
+            void *args[] = {(void *)&base, (void *)&nrows, (void *)&img, (void *)&fold, (void *)&out};
+            if (int rc = herr(hipLaunchKernel(small_fn(gl, prio), dim3(grid), dim3(64 * waves), args, 0, s)))
+                return rc;
             if (int rc = herr(hipGetLastError()))
                 return rc;
         }

@@ -71,10 +71,11 @@ def ctx_noprio(torch_cuda):
     c.close()
 
 
-@pytest.mark.parametrize("bs", [1024, 3072, 4096, 8192, 65536, 131072, 262144, 1 << 20])
+@pytest.mark.parametrize("bs", [16, 32, 64, 128, 256, 512, 1024, 3072, 4096, 8192, 65536, 131072, 262144, 1 << 20])
 def test_progress_priority_on_and_off(torch_cuda, ctx, ctx_noprio, bs):
-    """Every rows plan with and without its progress-priority mode: the same
-    CRCs as the oracle (priority only reorders instruction issue)."""
+    """Every rows plan and the sub-KiB kernel with and without progress
+    priority (and, sub-KiB, its 16-wave shape): the same CRCs as the oracle
+    (priority only reorders instruction issue)."""
     torch = torch_cuda
     nb = max(1, (48 << 20) // bs) + 3
     t = _region(torch, ctx, bs * nb, SEED ^ (bs * 7), nb)

@@ -272,14 +272,22 @@ static uint32_t *g_img8[65] = {};
 
 // sub-KiB blocks: crc_small_kernel<G> with the bit-matrix fold (OPT 0) against
 // the nibble fold (OPT 1), interleaved, bit-identity checked
-template <int G>
-void small_pair(const uint8_t *d, uint64_t nrows, const uint32_t *img, const uint32_t *fold, const uint32_t *nib,
-                uint32_t *o, uint32_t grid, int opt)
+// the sub-KiB variants compared by small_ab (OPT of crc_small_kernel)
+constexpr int kSmallOpts[] = {0, 1, 1 | 1024, 1 | 256 | 1024, 1 | 768 | 1024};
+constexpr int kSmallN = sizeof(kSmallOpts) / sizeof(kSmallOpts[0]);
+
+template <int G, int I = 0>
+void small_launch(int vi, const uint8_t *d, uint64_t nrows, const uint32_t *img, const uint32_t *fold,
+                  const uint32_t *nib, uint32_t *o, uint32_t grid)
 {
-    if (opt)
-        hipLaunchKernelGGL((crc_small_kernel<G, 1>), dim3(grid), dim3(kThreads), 0, 0, d, nrows, img, nib, o);
-    else
-        hipLaunchKernelGGL((crc_small_kernel<G, 0>), dim3(grid), dim3(kThreads), 0, 0, d, nrows, img, fold, o);
+    if constexpr (I < kSmallN) {
+        if (vi != I)
+            return small_launch<G, I + 1>(vi, d, nrows, img, fold, nib, o, grid);
+        constexpr int OPT = kSmallOpts[I];
+        const int nw = ext_waves(OPT);
+        hipLaunchKernelGGL((crc_small_kernel<G, OPT>), dim3(nw == 16 ? (grid + 1) / 2 : grid), dim3(64 * nw), 0, 0, d,
+                           nrows, img, (OPT & 1) ? nib : fold, o);
+    }
 }
 
 int small_ab(uint32_t bs, uint64_t nb, int rounds, int ncu)
@@ -305,41 +313,44 @@ int small_ab(uint32_t bs, uint64_t nb, int rounds, int ncu)
     const uint64_t nrows = nb / (1024 / bs);
     const uint64_t want = (nrows + 4 * kWaves - 1) / (4 * kWaves);
     const uint32_t grid = (uint32_t)std::min<uint64_t>(want, (uint64_t)ncu * 2);
-    auto run = [&](int opt) {
-        uint32_t *o = opt ? o1 : o0;
+    auto run = [&](int vi, uint32_t *o) {
         switch (G) {
-        case 2: small_pair<2>(d, nrows, d_img, d_fold, d_nib, o, grid, opt); break;
-        case 4: small_pair<4>(d, nrows, d_img, d_fold, d_nib, o, grid, opt); break;
-        case 8: small_pair<8>(d, nrows, d_img, d_fold, d_nib, o, grid, opt); break;
-        case 16: small_pair<16>(d, nrows, d_img, d_fold, d_nib, o, grid, opt); break;
-        default: small_pair<32>(d, nrows, d_img, d_fold, d_nib, o, grid, opt); break;
+        case 2: small_launch<2>(vi, d, nrows, d_img, d_fold, d_nib, o, grid); break;
+        case 4: small_launch<4>(vi, d, nrows, d_img, d_fold, d_nib, o, grid); break;
+        case 8: small_launch<8>(vi, d, nrows, d_img, d_fold, d_nib, o, grid); break;
+        case 16: small_launch<16>(vi, d, nrows, d_img, d_fold, d_nib, o, grid); break;
+        default: small_launch<32>(vi, d, nrows, d_img, d_fold, d_nib, o, grid); break;
         }
     };
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
-    std::vector<float> ms[2];
+    std::vector<float> ms[kSmallN];
+    bool same = true;
+    std::vector<uint32_t> a(nb), b(nb);
     for (int r = 0; r < rounds + 1; r++)
-        for (int opt = 0; opt < 2; opt++) {
+        for (int vi = 0; vi < kSmallN; vi++) {
+            uint32_t *o = vi ? o1 : o0;
             CK(hipEventRecord(e0, 0));
             for (int it = 0; it < 5; it++)
-                run(opt);
+                run(vi, o);
             CK(hipEventRecord(e1, 0));
             CK(hipEventSynchronize(e1));
             float t;
             CK(hipEventElapsedTime(&t, e0, e1));
             if (r)
-                ms[opt].push_back(t / 5);
+                ms[vi].push_back(t / 5);
+            else if (vi) {
+                CK(hipMemcpy(a.data(), o0, nb * 4, hipMemcpyDeviceToHost));
+                CK(hipMemcpy(b.data(), o1, nb * 4, hipMemcpyDeviceToHost));
+                same = same && !memcmp(a.data(), b.data(), nb * 4);
+            }
         }
-    std::vector<uint32_t> a(nb), b(nb);
-    CK(hipMemcpy(a.data(), o0, nb * 4, hipMemcpyDeviceToHost));
-    CK(hipMemcpy(b.data(), o1, nb * 4, hipMemcpyDeviceToHost));
-    const bool same = !memcmp(a.data(), b.data(), nb * 4);
-    for (int opt = 0; opt < 2; opt++) {
-        std::sort(ms[opt].begin(), ms[opt].end());
-        const double med = ms[opt][ms[opt].size() / 2];
-        printf("small G%d %-12s median %8.4f ms  %7.1f GB/s (best %7.1f)\n", G, opt ? "nibble-fold" : "bit-matrix", med,
-               (double)bs * nb / med / 1e6, (double)bs * nb / ms[opt][0] / 1e6);
+    for (int vi = 0; vi < kSmallN; vi++) {
+        std::sort(ms[vi].begin(), ms[vi].end());
+        const double med = ms[vi][ms[vi].size() / 2];
+        printf("small G%d opt%-5d median %8.4f ms  %7.1f GB/s (best %7.1f)\n", G, kSmallOpts[vi], med,
+               (double)bs * nb / med / 1e6, (double)bs * nb / ms[vi][0] / 1e6);
     }
     printf("small variants bit-identical: %s\n", same ? "yes" : "NO");
     return same ? 0 : 1;
