@@ -270,6 +270,24 @@ static uint32_t *g_img8[65] = {};
                                    img, g_nib[G], o, (uint32_t)(((WE) << 16) | (WO)));                         \
             }, {}}
 
+// one 16-wave workgroup per CU (OPT bit 10): grid = CUs, 1024 threads
+#define NIB16_VARIANT_W(G, CH, NB, AUX, OPT, WE, WO)                                                          \
+    Variant{"nib16w G" #G " CH" #CH " NBUF" #NB " AUX" #AUX " opt" #OPT " xw" #WE ":" #WO, true, G, CH, 1,      \
+            (OPT) | 1024,                                                                                      \
+            [](dim3 g, hipStream_t s, const uint8_t *b, uint64_t n, uint32_t bs, const uint32_t *img,           \
+               const uint32_t *, uint32_t *o) {                                                                \
+                hipLaunchKernelGGL((crc_rows_kernel<G, CH, NB, AUX, (OPT) | 32 | 1024>), g, dim3(1024), 0, s, b, n, \
+                                   bs, img, g_nib[G], o, (uint32_t)(((WE) << 16) | (WO)));                     \
+            }, {}}
+#define CRC16_VARIANT_W(G, CH, NB, AUX, OPT, WE, WO)                                                          \
+    Variant{"crc16w G" #G " CH" #CH " NBUF" #NB " AUX" #AUX " opt" #OPT " xw" #WE ":" #WO, true, G, CH, 1,      \
+            (OPT) | 1024,                                                                                      \
+            [](dim3 g, hipStream_t s, const uint8_t *b, uint64_t n, uint32_t bs, const uint32_t *img,           \
+               const uint32_t *fold, uint32_t *o) {                                                            \
+                hipLaunchKernelGGL((crc_rows_kernel<G, CH, NB, AUX, (OPT) | 1024>), g, dim3(1024), 0, s, b, n, bs,  \
+                                   img, fold, o, (uint32_t)(((WE) << 16) | (WO)));                             \
+            }, {}}
+
 // sub-KiB blocks: crc_small_kernel<G> with the bit-matrix fold (OPT 0) against
 // the nibble fold (OPT 1), interleaved, bit-identity checked
 // the sub-KiB variants compared by small_ab (OPT of crc_small_kernel)
@@ -424,6 +442,14 @@ int main(int argc, char **argv)
     all.push_back(NIB_VARIANT_W(64, 4, 2, 2, 1, 512, 31, 29));
     all.push_back(NIB_VARIANT_W(64, 4, 2, 2, 1, 768, 31, 29));
     all.push_back(NIB_VARIANT_W(32, 8, 2, 2, 1, 2 | 768, 8, 7));
+    all.push_back(NIB16_VARIANT_W(32, 8, 2, 2, 2 | 768, 31, 29));
+    all.push_back(NIB16_VARIANT_W(32, 8, 2, 2, 2 | 256, 31, 29));
+    all.push_back(NIB16_VARIANT_W(32, 8, 2, 2, 2, 31, 29));
+    all.push_back(NIB16_VARIANT_W(16, 4, 2, 2, 2 | 256, 31, 29));
+    all.push_back(NIB16_VARIANT_W(16, 4, 2, 2, 2 | 768, 31, 29));
+    all.push_back(CRC16_VARIANT_W(16, 4, 2, 2, 256, 31, 29));
+    all.push_back(CRC16_VARIANT_W(64, 4, 2, 2, 256, 31, 29));
+    all.push_back(CRC16_VARIANT_W(64, 4, 2, 2, 768, 31, 29));
     all.push_back(NIB_VARIANT_W(16, 4, 2, 2, 2, 2 | 256, 31, 29));
     all.push_back(NIB_VARIANT_W(16, 4, 2, 2, 2, 2 | 512, 31, 29));
     all.push_back(NIB_VARIANT_W(16, 4, 2, 2, 2, 2 | 768, 31, 29));
