@@ -59,6 +59,7 @@ struct priskv_crc_ctx {
     uint32_t plan_xw[8];       // rows-kernel split per plan: (even << 16) | odd XCD weight, 0 = equal
     int segment;               // split few large blocks / extents into segments (PRISKV_CRC_SEGMENT=0: off)
     int prio;                  // rows kernel progress priority (PRISKV_CRC_PRIO=0: off)
+    int balance;               // byte-balanced extents split (PRISKV_CRC_BALANCE=0: off)
     uint64_t seg_max_extents;  // device-resident lengths: segment calls of at most this many extents
     uint32_t *d_lds_image[3];  // 64 KiB each: set B gap for G = 64, 32, 16
     uint32_t *d_fold;          // kFoldSets x 2048 words, set j for G = 1 << j
@@ -168,8 +169,9 @@ constexpr int kExtWgPerCu = 2;            // ... and workgroups per CU (the same
 static_assert(ext_waves(kExtOpt) == kExtWaves && ext_waves(kExtOptMany) == kExtWaves * kExtWgPerCu,
               "both extents shapes hold 16 waves per CU");
 
-// many: the 16-wave shape (unless PRISKV_CRC_PRIO=0); seg: segmented items
-int launch_ext_kernel(const priskv_crc_ctx *ctx, bool seg, bool many, hipStream_t s, const uint8_t *abase,
+// many: the 16-wave shape (unless PRISKV_CRC_PRIO=0); seg: segmented items;
+// bal: byte-balanced split over prefix = the per-tile costs (two 8-wave shape)
+int launch_ext_kernel(const priskv_crc_ctx *ctx, bool seg, bool many, bool bal, hipStream_t s, const uint8_t *abase,
                       uint64_t n, const uint64_t *offs, const uint32_t *lens, uint64_t shift, uint64_t stride,
                       uint32_t len_const, uint32_t *out, const uint32_t *prefix, const uint8_t *shifts,
                       const uint32_t *zpow, uint32_t *sub)
@@ -188,6 +190,8 @@ int launch_ext_kernel(const priskv_crc_ctx *ctx, bool seg, bool many, hipStream_
     const void *fn;
     if (seg)
         fn = reinterpret_cast<const void *>(&crc_ranges_kernel<kExtRows, kNbuf, kAux, kExtOpt | 4>);
+    else if (bal && !many)
+        fn = reinterpret_cast<const void *>(&crc_ranges_kernel<kExtRows, kNbuf, kAux, kExtOpt | 2048>);
     else if (many)
         fn = reinterpret_cast<const void *>(&crc_ranges_kernel<kExtRows, kNbuf, kAux, kExtOptMany>);
     else
@@ -214,8 +218,25 @@ int launch_extents(const priskv_crc_ctx *ctx, const uint8_t *base, uint64_t n, c
         return 0;
     const uint64_t shift = (uintptr_t)base & 15;
     const uint8_t *abase = base - shift;
-    const bool many = n >= kExtManyPerWave * (uint64_t)ctx->num_cus * kExtWgPerCu * kExtWaves;
-    return launch_ext_kernel(ctx, false, many, s, abase, n, offs, lens, shift, stride, len_const, out, nullptr,
+    const uint64_t waves = (uint64_t)ctx->num_cus * kExtWgPerCu * kExtWaves;
+    const bool many = n >= kExtManyPerWave * waves;
+    // a few extents per wave: split by bytes, not counts, when
+    // the lengths vary (device arrays) and the tile sums fit one wave's scan
+    const uint64_t ntiles = (n + kExtTile - 1) / kExtTile;
+    if (ctx->balance && offs && !many && n >= waves && ntiles <= 64ull * kExtTileLanes) {
+        uint32_t *tiles = nullptr;
+        if (int rc = herr(hipMallocAsync((void **)&tiles, ntiles * sizeof(uint32_t), s)))
+            return rc;
+        hipLaunchKernelGGL(crc_ext_cost_kernel, dim3((uint32_t)((ntiles + 3) / 4)), dim3(256), 0, s, lens, n, tiles,
+                           ntiles);
+        int rc = herr(hipGetLastError());
+        if (!rc)
+            rc = launch_ext_kernel(ctx, false, false, true, s, abase, n, offs, lens, shift, stride, len_const, out,
+                                   tiles, nullptr, nullptr, nullptr);
+        const int frc = herr(hipFreeAsync(tiles, s));
+        return rc ? rc : frc;
+    }
+    return launch_ext_kernel(ctx, false, many, false, s, abase, n, offs, lens, shift, stride, len_const, out, nullptr,
                              nullptr, nullptr, nullptr);
 }
 
@@ -403,7 +424,7 @@ int launch_extents_seg(const priskv_crc_ctx *ctx, const uint8_t *base, uint64_t 
     int rc = herr(hipGetLastError());
     if (!rc) {
         const uint64_t sh = (uintptr_t)base & 15;
-        rc = launch_ext_kernel(ctx, true, false, s, base - sh, n, offs, lens, sh, stride, len_const, out, prefix, shifts,
+        rc = launch_ext_kernel(ctx, true, false, false, s, base - sh, n, offs, lens, sh, stride, len_const, out, prefix, shifts,
                                ctx->d_zpow, sub);
     }
     if (!rc) {
@@ -600,6 +621,8 @@ int priskv_crc_ctx_create(int device, priskv_crc_ctx **out)
         c->segment = !(e && !strcmp(e, "0"));
         const char *pe = getenv("PRISKV_CRC_PRIO");
         c->prio = !(pe && !strcmp(pe, "0"));
+        const char *be = getenv("PRISKV_CRC_BALANCE");
+        c->balance = !(be && !strcmp(be, "0"));
         c->seg_max_extents = kSegMaxExtents;
         if (const char *m = getenv("PRISKV_CRC_SEG_MAX_EXTENTS")) { // capped by the plan kernel's 16384
             const unsigned long long v = strtoull(m, nullptr, 10);

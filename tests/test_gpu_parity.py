@@ -478,6 +478,50 @@ def test_ranges_beyond_2GiB_and_many_per_wave(torch_cuda, ctx):
     del t
 
 
+@pytest.fixture(scope="module")
+def ctx_nobal(torch_cuda):
+    """A context with the byte-balanced extents split off (PRISKV_CRC_BALANCE=0)."""
+    import os
+    from priskv_amd import CrcContext
+    os.environ["PRISKV_CRC_BALANCE"] = "0"
+    try:
+        c = CrcContext(0)
+    finally:
+        del os.environ["PRISKV_CRC_BALANCE"]
+    yield c
+    c.close()
+
+
+@pytest.mark.parametrize("k", [4096, 4097, 20000, 65536, 131071])
+def test_ranges_balanced_split(torch_cuda, ctx, ctx_nobal, k):
+    """A few extents per wave with very uneven lengths (0 B to 256 KiB): the
+    byte-balanced split (crc_ext_cost_kernel + ext_boundary) must give every
+    extent to exactly one wave -- the output is pre-filled with a sentinel,
+    so a gap would show -- and the same CRCs as the count split and the
+    oracle.  k spans one extent per wave to just below the 16-wave shape."""
+    torch = torch_cuda
+    n = 512 << 20
+    t = _region(torch, ctx, n, SEED, 31)
+    rng = np.random.default_rng(k)
+    big = rng.random(k) < 0.05
+    lens = np.where(big, rng.integers(64 << 10, 256 << 10, k), rng.integers(0, 6000, k)).astype(np.uint32)
+    if k > 131000:
+        lens = np.minimum(lens, 12000).astype(np.uint32)  # keep the oracle pass short
+    lens[:4] = [0, 1, 256 << 10, 17]
+    offs = rng.integers(0, n - (256 << 10), k).astype(np.uint64)
+    d_o = torch.from_numpy(offs.astype(np.int64)).cuda()
+    d_l = torch.from_numpy(lens.view(np.int32)).cuda()
+    want = O.crc32_ranges(t[:n].cpu().numpy(), offs, lens)
+    sentinel = int(np.int32(np.uint32(0xA5A5A5A5).view(np.int32)))
+    for c in (ctx, ctx_nobal):
+        out = torch.full((k,), sentinel, dtype=torch.int32, device="cuda")
+        c.ranges_dev(t, d_o, d_l, out=out)
+        torch.cuda.synchronize()
+        got = _u32(out)
+        assert np.array_equal(got, want), (k, np.nonzero(got != want)[0][:8])
+    del t
+
+
 def test_ranges_many_per_wave_shapes(torch_cuda, any_ctx):
     """Enough extents (>= 32 per resident wave) for the extents kernel's
     16-wave progress-priority shape, with ragged offsets and lengths 0-9000 B,
