@@ -429,7 +429,8 @@ int launch_extents_seg(const priskv_crc_ctx *ctx, const uint8_t *base, uint64_t 
     }
     if (!rc) {
         const uint32_t grid = (uint32_t)((n + 3) / 4);
-        hipLaunchKernelGGL(crc_seg_reduce_kernel, dim3(grid), dim3(256), 0, s, sub, prefix, n, out);
+        hipLaunchKernelGGL(crc_seg_reduce_kernel, dim3(grid), dim3(256), 0, s, sub, prefix, shifts,
+                           offs ? lens : nullptr, len_const, ctx->d_zpow, n, out);
         rc = herr(hipGetLastError());
     }
     const int frc = herr(hipFreeAsync(scr, s));
