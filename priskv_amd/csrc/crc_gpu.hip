@@ -394,6 +394,7 @@ int launch_rows_plain(const priskv_crc_ctx *ctx, const uint8_t *base, uint64_t n
 // profiles/r01/seg_limit.jsonl); KV-cache values are the large kind.
 // PRISKV_CRC_SEG_MAX_EXTENTS moves the threshold (0 = never for device lengths).
 constexpr uint64_t kSegMaxExtents = 2048;
+constexpr uint64_t kSegPerWave = 8; // full segments per resident wave (tools/bench_paths.py few / ranges)
 constexpr uint32_t kSegMinLen = 64u << 10;
 
 int launch_extents_seg(const priskv_crc_ctx *ctx, const uint8_t *base, uint64_t n, const uint64_t *offs,
@@ -408,19 +409,21 @@ int launch_extents_seg(const priskv_crc_ctx *ctx, const uint8_t *base, uint64_t 
         return 0;
     if (max_len ? (max_len < kSegMinLen || balanced(n, waves)) : n > ctx->seg_max_extents)
         return 0;
-    uint32_t cap_log2 = 6; // >= 64 segments per extent allowed (16-64 KiB segments beat fewer, larger ones)
-    while (cap_log2 < 10 && (n << cap_log2) < 2 * waves)
-        cap_log2++;
+    // one segment size per call (crc_seg_plan_kernel): about kSegPerWave full
+    // segments per resident wave, so the count split of segments is a byte
+    // split; at most n + target segments, and segment distances d stay below
+    // 2^16 (the extents kernel's shift steps)
+    const uint64_t target = std::min<uint64_t>(kSegPerWave * waves, 32768);
     const size_t off_shift = ((n + 1) * 4 + 255) / 256 * 256;
     const size_t off_sub = off_shift + (n + 255) / 256 * 256;
     uint8_t *scr = nullptr;
-    if (int rc = herr(hipMallocAsync((void **)&scr, off_sub + (n << cap_log2) * 4, s)))
+    if (int rc = herr(hipMallocAsync((void **)&scr, off_sub + (n + target) * 4, s)))
         return rc;
     uint32_t *prefix = reinterpret_cast<uint32_t *>(scr);
     uint8_t *shifts = scr + off_shift;
     uint32_t *sub = reinterpret_cast<uint32_t *>(scr + off_sub);
-    hipLaunchKernelGGL(crc_seg_plan_kernel, dim3(1), dim3(kSegPlanThreads), 0, s, offs ? lens : nullptr, len_const, n, cap_log2,
-                       prefix, shifts);
+    hipLaunchKernelGGL(crc_seg_plan_kernel, dim3(1), dim3(kSegPlanThreads), 0, s, offs ? lens : nullptr, len_const, n,
+                       (uint32_t)target, prefix, shifts);
     int rc = herr(hipGetLastError());
     if (!rc) {
         const uint64_t sh = (uintptr_t)base & 15;
