@@ -263,12 +263,14 @@ struct Plan {
 };
 // opt = crc_rows_kernel OPT bits: 2 = pipelined fold, 32 = nibble-table fold,
 // (m << 8) = progress-priority mode m (profiles/r01/explore_*_prio*.log).
+// One workgroup per CU everywhere: the G16 plans gain 3-5 % from it over two
+// (profiles/r01/prio/occupancy_*.log).
 // Weights: swept per plan (profiles/r01/explore_*_xw*.log, bench_xw_ab.jsonl);
 // 31:29 is best or within noise for every plan in bench.py's sustained loop.
 constexpr int kPrio1 = 1 << 8, kPrio3 = 3 << 8;
 constexpr Plan kPlans[NPLANS] = {
-    {32, 8, 2 | 32 | kPrio3, 1, 31, 29}, {64, 4, 32 | kPrio1, 1, 31, 29}, {16, 4, 2 | 32 | kPrio1, 2, 31, 29},
-    {16, 4, kPrio1, 2, 31, 29},          {64, 4, kPrio1, 1, 31, 29},      {64, 4, kPrio3, 1, 31, 29},
+    {32, 8, 2 | 32 | kPrio3, 1, 31, 29}, {64, 4, 32 | kPrio1, 1, 31, 29}, {16, 4, 2 | 32 | kPrio1, 1, 31, 29},
+    {16, 4, kPrio1, 1, 31, 29},          {64, 4, kPrio1, 1, 31, 29},      {64, 4, kPrio3, 1, 31, 29},
     {64, 2, 0, 1, 31, 29},               {64, 1, 0, 1, 31, 29}};
 
 int plan_for(uint32_t bs)

@@ -451,10 +451,14 @@ int main(int argc, char **argv)
     all.push_back(CRC16_VARIANT_W(64, 4, 2, 2, 256, 31, 29));
     all.push_back(CRC16_VARIANT_W(64, 4, 2, 2, 768, 31, 29));
     all.push_back(NIB_VARIANT_W(16, 4, 2, 2, 2, 2 | 256, 31, 29));
+    all.push_back(NIB_VARIANT_W(16, 4, 2, 2, 1, 2, 31, 29));
+    all.push_back(NIB_VARIANT_W(16, 4, 2, 2, 1, 2 | 256, 31, 29));
     all.push_back(NIB_VARIANT_W(16, 4, 2, 2, 2, 2 | 512, 31, 29));
     all.push_back(NIB_VARIANT_W(16, 4, 2, 2, 2, 2 | 768, 31, 29));
     all.push_back(CRC_VARIANT_W(16, 4, 2, 2, 2, 0, 31, 29));
     all.push_back(CRC_VARIANT_W(16, 4, 2, 2, 2, 256, 31, 29));
+    all.push_back(CRC_VARIANT_W(16, 4, 2, 2, 1, 0, 31, 29));
+    all.push_back(CRC_VARIANT_W(16, 4, 2, 2, 1, 256, 31, 29));
     all.push_back(CRC_VARIANT_W(16, 4, 2, 2, 2, 768, 31, 29));
     all.push_back(CRC_VARIANT_W(64, 2, 2, 2, 1, 0, 31, 29));
     all.push_back(CRC_VARIANT_W(64, 2, 2, 2, 1, 256, 31, 29));
