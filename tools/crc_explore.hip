@@ -291,7 +291,7 @@ static uint32_t *g_img8[65] = {};
 // sub-KiB blocks: crc_small_kernel<G> with the bit-matrix fold (OPT 0) against
 // the nibble fold (OPT 1), interleaved, bit-identity checked
 // the sub-KiB variants compared by small_ab (OPT of crc_small_kernel)
-constexpr int kSmallOpts[] = {0, 1, 1 | 1024, 1 | 256 | 1024, 1 | 768 | 1024};
+constexpr int kSmallOpts[] = {0, 1, 1 | 1024, 1 | 256 | 1024, 1 | 768 | 1024, 1 | 256};
 constexpr int kSmallN = sizeof(kSmallOpts) / sizeof(kSmallOpts[0]);
 
 template <int G, int I = 0>
