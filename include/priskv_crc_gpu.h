@@ -46,7 +46,9 @@ typedef struct priskv_crc_ctx priskv_crc_ctx;
  * LDS images, nibble fold tables, shift matrices) and sizes the persistent
  * grid from the device's CU count.  *out is set only on success.
  * PRISKV_CRC_SEGMENT=0 in the environment at creation turns off the
- * segmentation of few large blocks / extents (measurement only). */
+ * segmentation of few large blocks / extents, PRISKV_CRC_PRIO=0 the
+ * kernels' progress priority and PRISKV_CRC_BALANCE=0 the byte-balanced
+ * extents split (measurement only). */
 int priskv_crc_ctx_create(int device, priskv_crc_ctx **out);
 void priskv_crc_ctx_destroy(priskv_crc_ctx *ctx);
 int priskv_crc_ctx_device(const priskv_crc_ctx *ctx);
@@ -66,8 +68,9 @@ int priskv_crc32_blocks_dev(const priskv_crc_ctx *ctx, const void *d_base, uint6
  * value_off (priskv_key, server/memory.h:50-51).  d_offsets / d_lengths /
  * d_out are device arrays of n entries.  Asynchronous on `stream`.  With few
  * extents (n <= 2048; PRISKV_CRC_SEG_MAX_EXTENTS) each is split into segments
- * on the device, which needs a small scratch allocation ordered on `stream`
- * (hipMallocAsync); -ENOMEM if that fails. */
+ * on the device; with a few extents per resident wave the split over the
+ * waves is balanced by bytes.  Both need a small scratch allocation ordered
+ * on `stream` (hipMallocAsync); -ENOMEM if that fails. */
 int priskv_crc32_ranges_dev(const priskv_crc_ctx *ctx, const void *d_base,
                             const uint64_t *d_offsets, const uint32_t *d_lengths, uint64_t n,
                             uint32_t *d_out, void *stream);
