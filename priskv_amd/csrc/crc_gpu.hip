@@ -433,8 +433,8 @@ int launch_extents_seg(const priskv_crc_ctx *ctx, const uint8_t *base, uint64_t 
                                ctx->d_zpow, sub);
     }
     if (!rc) {
-        const uint32_t grid = (uint32_t)((n + 3) / 4);
-        hipLaunchKernelGGL(crc_seg_reduce_kernel, dim3(grid), dim3(256), 0, s, sub, prefix, shifts,
+        const uint32_t grid = (uint32_t)n; // one workgroup per extent (n <= 16384)
+        hipLaunchKernelGGL(crc_seg_reduce_kernel, dim3(grid), dim3(kSegReduceThreads), 0, s, sub, prefix, shifts,
                            offs ? lens : nullptr, len_const, ctx->d_zpow, n, out);
         rc = herr(hipGetLastError());
     }
