@@ -67,7 +67,7 @@ int priskv_crc32_blocks_dev(const priskv_crc_ctx *ctx, const void *d_base, uint6
  * d_offsets[i], d_lengths[i]) -- a value of valuelen bytes starting at
  * value_off (priskv_key, server/memory.h:50-51).  d_offsets / d_lengths /
  * d_out are device arrays of n entries.  Asynchronous on `stream`.  With few
- * extents (n <= 2048; PRISKV_CRC_SEG_MAX_EXTENTS) each is split into segments
+ * extents (n <= 8192; PRISKV_CRC_SEG_MAX_EXTENTS) each is split into segments
  * on the device; with a few extents per resident wave the split over the
  * waves is balanced by bytes.  Both need a small scratch allocation ordered
  * on `stream` (hipMallocAsync); -ENOMEM if that fails. */

@@ -390,12 +390,15 @@ int launch_rows_plain(const priskv_crc_ctx *ctx, const uint8_t *base, uint64_t n
 // (one constant length on the blocks path, host arrays on the host scrub),
 // segment when the batch is unbalanced and that length is at least
 // kSegMinLen.  Device-resident lengths are unknown, so the rule uses the
-// count: at most kSegMaxExtents extents, half the resident waves.  At 2048
-// PrisKV-shaped values that costs small values ~16 us (4 KiB blocks: 10 ->
-// 26 us) and saves 0.5-0.8 ms on MiB values (1 MiB blocks: 1219 -> 747 us;
-// profiles/r01/seg_limit.jsonl); KV-cache values are the large kind.
+// count: at most kSegMaxExtents extents, twice the resident waves.  On the
+// current segmented path (one segment size per call) PrisKV-shaped values
+// at 8192 cost small values ~11 us (4 KiB blocks: 29 -> 40 us) and save
+// 0.65-0.75 ms on MiB values (1 MiB blocks, 4096: 1864 -> 1214 us, 8192:
+// 3252 -> 2498 us; 64 KiB blocks 209 -> 191 us); at 16384 the gain shrinks
+// to 5 % and small values lose 26 us (profiles/r01/seg_limit_r4g.jsonl).
+// KV-cache values are the large kind.
 // PRISKV_CRC_SEG_MAX_EXTENTS moves the threshold (0 = never for device lengths).
-constexpr uint64_t kSegMaxExtents = 2048;
+constexpr uint64_t kSegMaxExtents = 8192;
 constexpr uint64_t kSegPerWave = 8; // full segments per resident wave (tools/bench_paths.py few / ranges)
 constexpr uint32_t kSegMinLen = 64u << 10;
 
