@@ -120,6 +120,26 @@ def test_segmented_many_extents(torch_cuda, ctx_seg16k):
         assert np.array_equal(got, want), (k, np.nonzero(got != want)[0][:8])
 
 
+def test_segmentation_limit_boundary(torch_cuda, ctx):
+    """The default context segments device-length calls of up to 8192 extents
+    and not above: both sides of the boundary, ragged lengths incl. empty and
+    multi-MiB ones, give the oracle's CRCs."""
+    torch = torch_cuda
+    n_bytes = 128 << 20
+    t = _region(torch, ctx, n_bytes, SEED ^ 0x8192, 4)
+    host = t[:n_bytes].cpu().numpy()
+    rng = np.random.default_rng(8192)
+    for k in (8191, 8192, 8193):
+        lens = rng.integers(0, 70000, k).astype(np.uint32)
+        lens[:6] = [0, 1, 17, 3 << 20, 1 << 20, 65536]
+        offs = np.array([rng.integers(0, n_bytes - int(ln)) for ln in lens], dtype=np.uint64)
+        got = _u32(ctx.ranges_dev(t, torch.from_numpy(offs.astype(np.int64)).cuda(),
+                                  torch.from_numpy(lens.view(np.int32)).cuda()))
+        torch.cuda.synchronize()
+        want = O.crc32_ranges(host, offs, lens)
+        assert np.array_equal(got, want), (k, np.nonzero(got != want)[0][:8])
+
+
 @pytest.fixture(params=["segmented", "unsegmented", "no-priority"])
 def any_ctx(request, ctx, ctx_noseg, ctx_noprio):
     """The default context, one with segmentation off, and one with the
