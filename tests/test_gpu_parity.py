@@ -654,6 +654,57 @@ def test_stream_argument(torch_cuda, ctx):
     assert np.array_equal(_u32(out), O.crc32_blocks(t.cpu().numpy()[: bs * nb], bs, nthreads=8))
 
 
+@pytest.mark.parametrize("pool", ["1", "0"])
+def test_scratch_pool_across_streams(torch_cuda, pool):
+    """Calls that need scratch (segmented extents, segmented large blocks,
+    verify) enqueued back to back on three streams with no host sync between
+    them, with growing sizes: pooled slots pass from stream to stream ordered
+    only by their events (PRISKV_CRC_SCRATCH_POOL=0: per-call alloc/free).
+    Every output must equal the oracle's."""
+    import os
+    torch = torch_cuda
+    from priskv_amd import CrcContext
+    os.environ["PRISKV_CRC_SCRATCH_POOL"] = pool
+    try:
+        c = CrcContext(0)
+    finally:
+        del os.environ["PRISKV_CRC_SCRATCH_POOL"]
+    try:
+        nbytes = 96 << 20
+        region = _region(torch, c, nbytes, SEED ^ 0x9001, 2)
+        torch.cuda.synchronize()
+        host = region[:nbytes].cpu().numpy()
+        rng = np.random.default_rng(9001)
+        streams = [torch.cuda.Stream() for _ in range(3)]
+        calls = []
+        for i in range(18):
+            k = 1 + i % 6
+            lens = rng.integers(1 << 20, 12 << 20, k).astype(np.uint32)
+            offs = np.array([rng.integers(0, nbytes - int(ln)) for ln in lens], dtype=np.uint64)
+            calls.append((offs, lens, torch.from_numpy(offs.astype(np.int64)).cuda(),
+                          torch.from_numpy(lens.view(np.int32)).cuda()))
+        want = [O.crc32_ranges(host, o, ln) for o, ln, _, _ in calls]
+        bs_big = 16 << 20
+        want_blocks = O.crc32_blocks(host[: bs_big * 4], bs_big, nthreads=4)
+        torch.cuda.synchronize()
+        outs = []
+        for i, (o, ln, d_o, d_l) in enumerate(calls):
+            st = streams[i % 3]
+            with torch.cuda.stream(st):
+                a = c.ranges_dev(region, d_o, d_l, stream=st)
+                b = c.blocks_dev(region, bs_big, nblocks=1 + i % 4, stream=st)
+                exp = torch.from_numpy(want[i].view(np.int32)).to("cuda", non_blocking=False)
+                v = c.verify_dev(region, d_o, d_l, exp, stream=st)
+            outs.append((a, b, v))
+        torch.cuda.synchronize()
+        for i, (a, b, v) in enumerate(outs):
+            assert np.array_equal(_u32(a), want[i]), (pool, i)
+            assert np.array_equal(_u32(b), want_blocks[: 1 + i % 4]), (pool, i)
+            assert int(v[0]) == 0 and int(v[1]) == -1, (pool, i, v.tolist())
+    finally:
+        c.close()
+
+
 def test_concurrent_streams_and_threads(torch_cuda, ctx):
     """One context shared by 4 host threads, each on its own stream, each
     mixing calls that need stream-ordered scratch (segmented extents, segmented
