@@ -6,21 +6,32 @@ block of this GPU's shard, device-resident (inputs already in HBM when the
 timed region starts), through the library's C ABI
 (priskv_crc32_blocks_dev, include/priskv_crc_gpu.h).
 
-Default workload (BASELINE.json configs[1]): 1 Mi x 4 KiB blocks = 4 GiB per
-GPU.  For N > 1 (launched by torch.distributed.run) each rank owns its own
-4 GiB shard -- the next 1 Mi blocks of one global region -- and checksums it
-with no data-path collective ("weak" scaling); the barrier and the max-over-
-ranks reduction are the benchmark contract, not part of the path.
+Headline workload (`value`, BASELINE.json configs[1]): 1 Mi x 4 KiB blocks =
+4 GiB per GPU.  For N > 1 (launched by torch.distributed.run) each rank owns
+its own 4 GiB shard -- the next 1 Mi blocks of one global region -- and
+checksums it with no data-path collective ("weak" scaling); the barrier and
+the max-over-ranks reduction are the benchmark contract, not part of the path.
 
-Prints ONE JSON line on rank 0.  Extra keys:
+Extra keys of the ONE JSON line rank 0 prints:
+  tib           BASELINE.json configs[3] measured in the same run at every N:
+                each rank's shard of the 16 Mi x 64 KiB (1 TiB at 8 GPUs)
+                region, 2 Mi x 64 KiB = 128 GiB per GPU, filled on the device;
+                aggregate GiB/s over the N ranks (barrier + max over ranks),
+                with sampled blocks (first, last, every 4096th of every
+                shard) checked bit-exactly against the CPU oracle
   roofline      dominant kernel (crc_rows_kernel) vs the HBM roof: algorithmic
                 bytes per launch / average launch time (HIP events on the launch
                 stream); traffic = PMC-measured HBM bytes per launch for this
                 workload when profiles/ holds a matching measurement, else null
-  cpu_baseline  rank 0 at N=1: the reference's own server/crc.c (compiled -O2
-                into oracle/_ref) timed single-threaded on a bounded sample of
-                the same blocks, which also serves as a bit-exact spot check
-  cpu_baseline_threads  the same sample split over 16 threads (the box's CPU share)
+  cold_ms       the first full pass after the device has idled (clock ramp
+                included), beside the steady-state `value`
+  pipelined     the same K passes round-robin on 2 streams (reported beside,
+                never instead of, `value`)
+  cpu_baseline  rank 0, every N, after all GPU work: the reference's own
+                server/crc.c (compiled unmodified into oracle/_ref at -O2, its
+                release flag, and -O0, the shipped default) timed on a bounded
+                sample of the same blocks, 1 thread and every thread this
+                process may use; the CRCs double as a bit-exact spot check
   parity        result of comparing the GPU CRCs with those CPU samples
 """
 from __future__ import annotations
@@ -40,14 +51,16 @@ METRIC = "GiB/s CRC over device-resident value blocks at 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
 SEED = 0x5EED5EED
 RAMP_S = 0.3
+COLD_IDLE_S = 1.0
 
 CONFIGS = {
     # name: (block_size, nblocks per GPU, description)
-    "default": (4096, 1 << 20, "1Mi x 4KiB value blocks per GPU, device-resident (4 GiB/GPU)"),
+    "default": (4096, 1 << 20, "1Mi x 4KiB value blocks per GPU, device-resident (4 GiB/GPU; BASELINE configs[1])"),
     "sweep64k": (65536, 1 << 16, "64Ki x 64KiB value blocks per GPU, device-resident (4 GiB/GPU)"),
     "sweep1m": (1 << 20, 1 << 12, "4Ki x 1MiB value blocks per GPU, device-resident (4 GiB/GPU)"),
-    "tib": (65536, 1 << 21, "2Mi x 64KiB value blocks per GPU (128 GiB/GPU; 1 TiB at 8 GPUs)"),
+    "tib": (65536, 1 << 21, "2Mi x 64KiB value blocks per GPU (128 GiB/GPU; 1 TiB at 8 GPUs; BASELINE configs[3])"),
 }
+TIB_BS, TIB_NB = CONFIGS["tib"][0], CONFIGS["tib"][1]
 
 
 def parse():
@@ -58,15 +71,17 @@ def parse():
     p.add_argument("--config", default="default", choices=sorted(CONFIGS) + ["streamed"])
     p.add_argument("--block-size", type=int, default=None)
     p.add_argument("--nblocks", type=int, default=None)
-    p.add_argument("--cpu-sample-bytes", type=int, default=3 << 30,
-                   help="bytes of the shard the CPU baseline hashes (about 10 s at -O2)")
+    p.add_argument("--cpu-sample-bytes", type=int, default=2 << 30,
+                   help="bytes of the shard the single-thread CPU baselines hash (about 4 s at -O2)")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-tib", action="store_true", help="skip the configs[3] (128 GiB/GPU) leg")
+    p.add_argument("--tib-steps", type=int, default=10)
     p.add_argument("--pipeline-streams", type=int, default=2,
                    help="streams for the reported-beside pipelined pass (0 = skip it)")
     return p.parse_args()
 
 
-def load_traffic(cfg_name: str, block_size: int, nblocks: int):
+def load_traffic(block_size: int, nblocks: int):
     """HBM bytes per launch from a committed rocprofv3 PMC summary, if one matches."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
@@ -76,6 +91,31 @@ def load_traffic(cfg_name: str, block_size: int, nblocks: int):
         return None if e is None else float(e["hbm_bytes_per_launch"])
     except (OSError, ValueError, KeyError):
         return None
+
+
+def cpu_threads():
+    """(threads used, CPUs in this process's affinity mask).  The box exports
+    OMP_NUM_THREADS = its CPU share; the affinity mask may list the whole host."""
+    avail = len(os.sched_getaffinity(0))
+    try:
+        cap = int(os.environ.get("OMP_NUM_THREADS", "0"))
+    except ValueError:
+        cap = 0
+    return (min(avail, cap) if cap > 0 else avail), avail
+
+
+def ramp(fn, sync):
+    """The first ~10 launches after idle run up to 40 % slow while the device
+    leaves its idle power state (profiles/r01/clock_ramp.txt): keep stepping,
+    untimed, until RAMP_S seconds of back-to-back work have passed."""
+    n = 0
+    t_r = time.perf_counter()
+    while time.perf_counter() - t_r < RAMP_S:
+        for _ in range(4):
+            fn(n)
+            n += 1
+        sync()
+    return n
 
 
 def main():
@@ -119,48 +159,54 @@ def main():
     ctx.fill_splitmix(region, SEED, word_offset=shard_word_offset(first, bs))
     out = torch.empty(nb, dtype=torch.int32, device=dev)
     stream = torch.cuda.current_stream()
-    torch.cuda.synchronize()
-
-    for _ in range(args.warmup):
-        ctx.blocks_dev(region, bs, out=out, stream=stream)
-    torch.cuda.synchronize()
-    # The first ~10 launches after idle run up to 40% slow while the device
-    # leaves its idle power state (profiles/r01/clock_ramp.txt); keep stepping,
-    # untimed, until >= RAMP_S seconds of back-to-back work have passed so the
-    # timed steps see steady-state serving throughput.
-    ramp = 0
-    t_r = time.perf_counter()
-    while time.perf_counter() - t_r < RAMP_S:
-        for _ in range(8):
-            ctx.blocks_dev(region, bs, out=out, stream=stream)
-        torch.cuda.synchronize()
-        ramp += 8
+    sync = torch.cuda.synchronize
 
     def barrier():
         if world > 1:
             dist.barrier()
+
+    def step(_i=0):
+        ctx.blocks_dev(region, bs, out=out, stream=stream)
+
+    # cold pass: the kernel's code object is loaded by a small call first,
+    # then the device idles COLD_IDLE_S and ONE full pass is timed -- what a
+    # one-off recovery scrub sees (clock ramp included)
+    ctx.blocks_dev(region, bs, out=out, stream=stream, nblocks=min(nb, 64))
+    sync()
+    time.sleep(COLD_IDLE_S)
+    ec0, ec1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ec0.record(stream)
+    step()
+    ec1.record(stream)
+    sync()
+    cold_ms = ec0.elapsed_time(ec1)
+
+    for _ in range(args.warmup):
+        step()
+    sync()
+    nramp = ramp(step, sync)
 
     trace = os.environ.get("PRISKV_BENCH_TRACE")
     if trace:  # per-step kernel times of a separate, untimed pass (diagnostics only)
         evs = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
         evs[0].record(stream)
         for i in range(args.steps):
-            ctx.blocks_dev(region, bs, out=out, stream=stream)
+            step()
             evs[i + 1].record(stream)
-        torch.cuda.synchronize()
+        sync()
         print("per-step ms:", " ".join(f"{evs[i].elapsed_time(evs[i + 1]):.3f}" for i in range(args.steps)),
               file=sys.stderr)
 
     ev0 = torch.cuda.Event(enable_timing=True)
     ev1 = torch.cuda.Event(enable_timing=True)
     barrier()
-    torch.cuda.synchronize()
+    sync()
     t0 = time.perf_counter()
     ev0.record(stream)
     for _ in range(args.steps):
-        ctx.blocks_dev(region, bs, out=out, stream=stream)
+        step()
     ev1.record(stream)
-    torch.cuda.synchronize()
+    sync()
     barrier()
     t1 = time.perf_counter()
     elapsed = t1 - t0
@@ -172,7 +218,7 @@ def main():
     value = total_bytes * args.steps / elapsed_max / 2**30
     alg_bytes = nb * (bs + 4)  # block read + 4-byte CRC written
     achieved = alg_bytes / (kernel_ms * 1e-3) / 1e9
-    traffic = load_traffic(args.config, bs, nb)
+    traffic = load_traffic(bs, nb)
     path = ctx_path(bs, region)
 
     result = {
@@ -190,31 +236,38 @@ def main():
         "data": "synthetic (splitmix64 pattern filled on device)",
         "config": {"workload": desc, "block_size": bs, "nblocks_per_gpu": nb,
                    "bytes_per_gpu": bs * nb, "parallelism": f"shard{world} (contiguous block ranges, no collective)",
-                   "kernel": path, "untimed_ramp_launches": ramp},
+                   "kernel": path, "untimed_ramp_launches": nramp,
+                   "also_measured": None if args.no_tib else CONFIGS["tib"][2] + " -> `tib`"},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": traffic, "kernel_ms": round(kernel_ms, 4),
                      "alg_bytes_per_launch": alg_bytes},
+        "cold_ms": round(cold_ms, 4),
+        "cold": {"ms": round(cold_ms, 4), "value": round(bs * nb / (cold_ms * 1e-3) / 2**30, 2), "unit": "GiB/s",
+                 "note": f"rank-local first pass after {COLD_IDLE_S:.1f} s idle (kernel already loaded)"},
     }
 
     if args.pipeline_streams > 1:
         # Reported beside `value`, never instead of it: the same K batch
         # passes, issued round-robin over independent streams as a server
         # with several scrub/verify batches in flight would.  Kernels on one
-        # stream are serialized, so every batch pays its own tail (the last
-        # ~50 us below the HBM rate); on separate streams the next
-        # batch's workgroups take the CUs that the previous one frees.
+        # stream are serialized, so every batch pays its own tail;
+        # on separate streams the next batch's workgroups take the CUs that
+        # the previous one frees.  It gets the same untimed ramp as `value`.
         ns = args.pipeline_streams
         pstreams = [stream] + [torch.cuda.Stream(device=dev) for _ in range(ns - 1)]
         pouts = [out] + [torch.empty(nb, dtype=torch.int32, device=dev) for _ in range(ns - 1)]
-        for i in range(2 * ns):
+
+        def pstep(i):
             ctx.blocks_dev(region, bs, out=pouts[i % ns], stream=pstreams[i % ns])
+
+        ramp(pstep, sync)
         barrier()
-        torch.cuda.synchronize()
+        sync()
         tp0 = time.perf_counter()
         for i in range(args.steps):
-            ctx.blocks_dev(region, bs, out=pouts[i % ns], stream=pstreams[i % ns])
-        torch.cuda.synchronize()
+            pstep(i)
+        sync()
         barrier()
         p_elapsed = max_over_ranks(time.perf_counter() - tp0, device=dev)
         same = all(torch.equal(pouts[0], o) for o in pouts[1:])
@@ -223,72 +276,147 @@ def main():
                                "frac_of_peak": round(alg_bytes * args.steps / p_elapsed / 1e9 / HBM_PEAK_GBS, 4),
                                "outputs_identical": bool(same)}
 
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        sys.path.insert(0, os.path.join(ROOT, "tests"))
-        import _oracle as O
-        nsamp = max(1, min(nb, args.cpu_sample_bytes // bs))
-        host = region[: nsamp * bs].cpu().numpy()
-        secs, cpu_crc, kind, label = O.time_cpu_baseline(host, bs)
-        gpu_crc = as_u32(out[:nsamp])
-        ok = bool(np.array_equal(cpu_crc, gpu_crc))
-        result["cpu_baseline"] = {"value": round(nsamp * bs / secs / 2**30, 4), "unit": "GiB/s", "cores": 1,
-                                  "kind": kind,
-                                  "sample": f"first {nsamp} x {bs} B blocks ({nsamp * bs / 2**30:.2f} GiB) of the "
-                                            f"same shard, 1 thread, {label}; {secs:.1f} s",
-                                  "cpu": cpu_model()}
-        # the same sample split over the box's CPU share (SURVEY 8(d) config 1
-        # asks for 1 thread and all threads); reported beside, not instead
-        nthr = int(os.environ.get("PRISKV_BENCH_CPU_THREADS", "16"))
-        secs_mt, cpu_crc_mt, _, _ = O.time_cpu_baseline(host, bs, threads=nthr)
-        ok = ok and bool(np.array_equal(cpu_crc_mt, gpu_crc))
-        result["cpu_baseline_threads"] = {"value": round(nsamp * bs / secs_mt / 2**30, 4), "unit": "GiB/s",
-                                          "cores": nthr, "kind": kind,
-                                          "sample": f"same sample, {nthr} threads (static block split); "
-                                                    f"{secs_mt:.2f} s"}
-        result["parity"] = {"checked_blocks": nsamp, "bit_exact": ok}
-        if not ok:
-            bad = np.nonzero(cpu_crc != gpu_crc)[0]
-            result["parity"]["first_mismatch"] = int(bad[0])
-    elif world > 1:
-        # every rank spot-checks the start of its own shard against the oracle
-        # (untimed); the flags are min-reduced so rank 0 reports all ranks
-        sys.path.insert(0, os.path.join(ROOT, "tests"))
-        import _oracle as O
-        nsamp = max(1, min(nb, (64 << 20) // bs))
-        ok = np.array_equal(O.crc32_blocks(region[: nsamp * bs].cpu().numpy(), bs, nthreads=8), as_u32(out[:nsamp]))
-        all_ok = max_over_ranks(0.0 if ok else 1.0, device=dev) == 0.0
-        result["parity"] = {"checked_blocks_per_rank": nsamp, "bit_exact": bool(all_ok)}
+    # every rank checks a sample of its own shard against the oracle
+    # (untimed); the CPU baseline times the reference on rank 0's sample
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import _oracle as O
+    want_cpu = rank == 0 and not args.no_cpu_baseline
+    nsamp = max(1, min(nb, (args.cpu_sample_bytes if want_cpu else 64 << 20) // bs))
+    host = region[: nsamp * bs].cpu().numpy()
+    gpu_crc = as_u32(out[:nsamp])
+    del region
+    torch.cuda.empty_cache()
+
+    if not args.no_tib:
+        result["tib"] = tib_leg(args, torch, ctx, dev, rank, world, barrier, O)
+
+    ok = bool(np.array_equal(O.crc32_blocks(host, bs, nthreads=8), gpu_crc))
+    all_ok = max_over_ranks(0.0 if ok else 1.0, device=dev) == 0.0
+    result["parity"] = {"checked_blocks_per_rank": nsamp, "bit_exact": bool(all_ok), "oracle": "oracle/crc_oracle.c"}
+    if want_cpu:
+        result["cpu_baseline"], cpu_ok = cpu_baseline(O, host, bs, gpu_crc)
+        result["parity"]["bit_exact_vs_reference_build"] = cpu_ok
+    barrier()
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:
         dist.destroy_process_group()
 
 
+def tib_leg(args, torch, ctx, dev, rank, world, barrier, O):
+    """BASELINE configs[3]: this rank's 2 Mi x 64 KiB (128 GiB) shard of the
+    16 Mi x 64 KiB region (world ranks x 2 Mi blocks), filled on the device."""
+    from priskv_amd import as_u32
+    from priskv_amd.shard import max_over_ranks, shard_blocks, shard_word_offset
+    bs = TIB_BS
+    first, nb = shard_blocks(world * TIB_NB, rank, world)
+    try:
+        region = torch.empty(bs * nb, dtype=torch.uint8, device=dev)
+    except torch.OutOfMemoryError as e:  # reported, never silently shrunk
+        return {"skipped": f"cannot allocate {bs * nb / 2**30:.0f} GiB: {e}"}
+    ctx.fill_splitmix(region, SEED, word_offset=shard_word_offset(first, bs))
+    out = torch.empty(nb, dtype=torch.int32, device=dev)
+    stream = torch.cuda.current_stream()
+
+    def step(_i=0):
+        ctx.blocks_dev(region, bs, out=out, stream=stream)
+
+    step()
+    torch.cuda.synchronize()
+    ramp(step, torch.cuda.synchronize)
+    k = max(1, args.tib_steps)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for _ in range(k):
+        step()
+    ev1.record(stream)
+    torch.cuda.synchronize()
+    barrier()
+    el = max_over_ranks(time.perf_counter() - t0, device=dev)
+    kms = ev0.elapsed_time(ev1) / k
+    # sampled parity: first and last block of the shard and every 4096th
+    # (the >2 GiB and >64 GiB ends of the shard included)
+    idx = np.unique(np.concatenate([np.arange(0, nb, 4096), [nb - 1]])).astype(np.int64)
+    ti = torch.from_numpy(idx).to(dev)
+    blocks = region.view(nb, bs).index_select(0, ti).cpu().numpy()
+    got = as_u32(out.index_select(0, ti))
+    want = O.crc32_blocks(blocks.reshape(-1), bs, nthreads=8)
+    ok = bool(np.array_equal(got, want))
+    all_ok = max_over_ranks(0.0 if ok else 1.0, device=dev) == 0.0
+    alg = nb * (bs + 4)
+    del region, out
+    torch.cuda.empty_cache()
+    return {"workload": CONFIGS["tib"][2], "value": round(bs * nb * world * k / el / 2**30, 2), "unit": "GiB/s",
+            "n_gpus": world, "steps": k, "ms_per_step": round(el / k * 1e3, 4), "bytes_per_gpu": bs * nb,
+            "kernel": ctx_path_bs(bs), "roofline": {"achieved": round(alg / (kms * 1e-3) / 1e9, 1),
+                                                      "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                                      "frac": round(alg / (kms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                                                      "kernel_ms": round(kms, 4)},
+            "parity": {"checked_blocks_per_rank": int(idx.size), "sample": "first, last, every 4096th block",
+                       "bit_exact": bool(all_ok)}}
+
+
+def cpu_baseline(O, host, bs, gpu_crc):
+    """The reference's server/crc.c at -O2 and -O0, 1 thread and every thread
+    this process may use, on the same sample (rank 0, after all GPU work)."""
+    nthr, avail = cpu_threads()
+    n1 = host.size // bs
+    variants, ok = [], True
+    top = None
+    for opt in ("O2", "O0"):
+        for thr in (1, nthr):
+            secs, crc, kind, label = O.time_cpu_baseline(host, bs, threads=thr, opt=opt)
+            ok = ok and bool(np.array_equal(crc, gpu_crc))
+            v = {"opt": f"-{opt}", "threads": thr, "value": round(n1 * bs / secs / 2**30, 4), "seconds": round(secs, 3),
+                 "kind": kind}
+            variants.append(v)
+            if opt == "O2" and thr == 1:
+                top = (v, kind, label)
+    v, kind, label = top
+    info = O.ref_build_info()
+    return ({"value": v["value"], "unit": "GiB/s", "cores": 1, "kind": kind,
+             "sample": f"first {n1} x {bs} B blocks ({n1 * bs / 2**30:.2f} GiB) of rank 0's shard; {label}; "
+                       f"variants = -O2 (PRISKV_RELEASE, server/Makefile:23-24) and -O0 (shipped default, "
+                       f"server/Makefile:25-26) at 1 and {nthr} threads (static block split)",
+             "variants": variants, "threads_used": nthr, "cpus_in_affinity": avail, "cpu": cpu_model(),
+             "compiler": info.get("compiler")}, ok)
+
+
+def ctx_path_bs(bs):
+    from priskv_amd import blocks_path
+    return rows_plan_name(bs) if blocks_path(16 << 10, 1, bs) == "rows" else f"crc_{blocks_path(16 << 10, 1, bs)}_kernel"
+
+
 def ctx_path(bs, region):
     """Kernel the library dispatches to (mirrors plan_for() in crc_gpu.hip)."""
     from priskv_amd import blocks_path
     p = blocks_path(region.data_ptr(), 1, bs)
-    if p == "rows":
-        pipe = bs in (1024, 4096)
-        if bs == 4096:
-            g, ch = 32, 8
-        elif bs <= 16384 and bs % 4096:
-            g, ch = 16, 4
-        else:
-            r = bs // 1024
-            g, ch = 64, (4 if r % 4 == 0 else (2 if r % 2 == 0 else 1))
-        w = os.environ.get("PRISKV_CRC_XCD_WEIGHTS", "31:29")
-        split = "" if w.replace(" ", "") in ("1:1",) else f",xcd-weighted {w}"
-        fold = ",pipelined-fold" if pipe else ""
-        if bs in (1024, 4096, 8192):
-            fold += ",nibble-table-fold"
-        # progress-priority mode of the plan (kPlans in crc_gpu.hip)
-        mode = 3 if bs == 4096 or (g == 64 and ch == 4 and bs >= 256 << 10) else (1 if ch == 4 or g == 16 else 0)
-        if os.environ.get("PRISKV_CRC_PRIO") == "0":
-            mode = 0
-        prio = f",progress-priority {mode}" if mode else ""
-        return f"crc_rows_kernel<G={g},CH={ch},NBUF=2,nt{fold}{split}{prio}>"
-    return f"crc_{p}_kernel"
+    return rows_plan_name(bs) if p == "rows" else f"crc_{p}_kernel"
+
+
+def rows_plan_name(bs):
+    pipe = bs in (1024, 4096)
+    if bs == 4096:
+        g, ch = 32, 8
+    elif bs <= 16384 and bs % 4096:
+        g, ch = 16, 4
+    else:
+        r = bs // 1024
+        g, ch = 64, (4 if r % 4 == 0 else (2 if r % 2 == 0 else 1))
+    w = os.environ.get("PRISKV_CRC_XCD_WEIGHTS", "31:29")
+    split = "" if w.replace(" ", "") in ("1:1",) else f",xcd-weighted {w}"
+    fold = ",pipelined-fold" if pipe else ""
+    if bs in (1024, 4096, 8192):
+        fold += ",nibble-table-fold"
+    # progress-priority mode of the plan (kPlans in crc_gpu.hip)
+    mode = 3 if bs == 4096 or (g == 64 and ch == 4 and bs >= 256 << 10) else (1 if ch == 4 or g == 16 else 0)
+    if os.environ.get("PRISKV_CRC_PRIO") == "0":
+        mode = 0
+    prio = f",progress-priority {mode}" if mode else ""
+    return f"crc_rows_kernel<G={g},CH={ch},NBUF=2,nt{fold}{split}{prio}>"
 
 
 def cpu_model():

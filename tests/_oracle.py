@@ -142,12 +142,23 @@ def splitmix_numpy(nwords: int, seed: int, word_offset: int = 0) -> np.ndarray:
     return z
 
 
-def time_cpu_baseline(region: np.ndarray, block_size: int, prefer: str = "reference", threads: int = 1):
+def ref_build_info() -> dict:
+    """oracle/_ref/BUILDINFO.json (compiler and flags of the reference build), or {}."""
+    import json
+    try:
+        with open(os.path.join(ORACLE_DIR, "_ref", "BUILDINFO.json")) as f:
+            return json.load(f)
+    except (OSError, ValueError):
+        return {}
+
+
+def time_cpu_baseline(region: np.ndarray, block_size: int, prefer: str = "reference", threads: int = 1,
+                      opt: str = "O2"):
     """Time a CPU pass over region's blocks in C (threads > 1: static split).
 
-    prefer="reference": the reference's own server/crc.c (oracle/_ref, -O2,
-    its release flag) when it was built; otherwise our restatement ("port").
-    Returns (seconds, crcs uint32[], kind, label)."""
+    prefer="reference": the reference's own server/crc.c (oracle/_ref, built at
+    -O2, its release flag, or -O0, its shipped default) when it was built;
+    otherwise our restatement ("port").  Returns (seconds, crcs uint32[], kind, label)."""
     L = lib()
     L.oracle_time_blocks_fn.restype = ctypes.c_double
     L.oracle_time_blocks_fn.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32,
@@ -155,10 +166,10 @@ def time_cpu_baseline(region: np.ndarray, block_size: int, prefer: str = "refere
     region = np.ascontiguousarray(region).view(np.uint8)
     n = region.size // block_size
     out = np.empty(n, dtype=np.uint32)
-    R = ref_lib("O2") if prefer == "reference" else None
+    R = ref_lib(opt) if prefer == "reference" else None
     if R is not None:
         fn = ctypes.cast(R.priskv_crc32, ctypes.c_void_p).value
-        kind, label = "reference", "server/crc.c priskv_crc32 compiled -O2 (oracle/_ref)"
+        kind, label = "reference", f"server/crc.c priskv_crc32 compiled -{opt} (oracle/_ref)"
     else:
         fn = ctypes.cast(L.oracle_crc32_u32len, ctypes.c_void_p).value
         kind, label = "port", "oracle/crc_oracle.c byte-serial restatement -O2"

@@ -879,3 +879,57 @@ def test_full_sweep_4GiB(torch_cuda, ctx, bs):
     torch.cuda.synchronize()
     want = O.crc32_blocks(t.cpu().numpy(), bs, nthreads=16)
     assert np.array_equal(_u32(out), want)
+
+
+@pytest.mark.slow
+def test_tib_config_per_gpu_shard(torch_cuda, ctx):
+    """BASELINE configs[3]: one GPU's 2 Mi x 64 KiB = 128 GiB shard of the
+    16 Mi x 64 KiB (1 TiB, 8-GPU) region, filled on the device exactly as
+    bench.py's `tib` leg fills rank 7's shard (word offset of block 14 Mi).
+
+    - sampled blocks vs the CPU oracle: first, last and every 4096th block
+      (offsets up to 128 GiB, so bit 31 .. bit 36 of the byte offset are set);
+    - full size, no oracle: combine consistency -- every 128 KiB block's CRC
+      equals combine(crc(first 64 KiB), crc(second 64 KiB), 64 KiB) from the
+      64 KiB batch of the same bytes (another plan, G64 over 128 rows);
+    - full size, no oracle: linearity (init 0 / xorout 0) -- XOR-ing the same
+      constant block C into every block XORs crc(C) into every CRC."""
+    from priskv_amd import crc32_shift
+    from priskv_amd.shard import shard_blocks, shard_word_offset
+    torch = torch_cuda
+    bs, per_gpu, world, rank = 65536, 1 << 21, 8, 7
+    first, nb = shard_blocks(world * per_gpu, rank, world)
+    t = torch.empty(bs * nb, dtype=torch.uint8, device="cuda")
+    ctx.fill_splitmix(t, SEED, shard_word_offset(first, bs))
+    c64 = ctx.blocks_dev(t, bs)
+    torch.cuda.synchronize()
+    idx = np.unique(np.concatenate([np.arange(0, nb, 4096), [1, nb - 2, nb - 1]])).astype(np.int64)
+    ti = torch.from_numpy(idx).cuda()
+    blocks = t.view(nb, bs).index_select(0, ti).cpu().numpy()
+    got = _u32(c64.index_select(0, ti))
+    want = O.crc32_blocks(blocks.reshape(-1), bs, nthreads=8)
+    assert np.array_equal(got, want), np.nonzero(got != want)[0][:8]
+    # the sampled bytes are the oracle generator's (the fill is pinned too)
+    assert np.array_equal(blocks[-1], O.fill_splitmix(bs, SEED, shard_word_offset(first + nb - 1, bs)))
+    # combine consistency over the whole shard
+    a = _u32(c64)
+    c128 = _u32(ctx.blocks_dev(t, 2 * bs))
+    torch.cuda.synchronize()
+    cols = np.array([crc32_shift(1 << i, bs) for i in range(32)], dtype=np.uint32)
+    lo = a[0::2]
+    sh = np.zeros_like(lo)
+    for i in range(32):
+        sh ^= np.where((lo >> np.uint32(i)) & np.uint32(1), cols[i], np.uint32(0)).astype(np.uint32)
+    assert np.array_equal(c128, sh ^ a[1::2])
+    # linearity over the whole shard, in place
+    C = O.fill_splitmix(bs, SEED ^ 0xC0FFEE, 3)
+    crc_c = O.crc32(C)
+    tv = t.view(nb, bs)
+    cd = torch.from_numpy(C).cuda()
+    for k in range(0, nb, 1 << 17):  # 8 GiB at a time keeps the temporaries small
+        tv[k:k + (1 << 17)].bitwise_xor_(cd)
+    cx = _u32(ctx.blocks_dev(t, bs))
+    torch.cuda.synchronize()
+    assert np.array_equal(cx, a ^ np.uint32(crc_c))
+    del t, tv, c64
+    torch.cuda.empty_cache()
