@@ -219,7 +219,7 @@ def main():
     alg_bytes = nb * (bs + 4)  # block read + 4-byte CRC written
     achieved = alg_bytes / (kernel_ms * 1e-3) / 1e9
     traffic = load_traffic(bs, nb)
-    path = ctx_path(bs, region)
+    path = ctx.blocks_plan(region.data_ptr(), nb, bs)  # the library reports its own plan
 
     result = {
         "metric": METRIC,
@@ -351,7 +351,7 @@ def tib_leg(args, torch, ctx, dev, rank, world, barrier, O):
     torch.cuda.empty_cache()
     return {"workload": CONFIGS["tib"][2], "value": round(bs * nb * world * k / el / 2**30, 2), "unit": "GiB/s",
             "n_gpus": world, "steps": k, "ms_per_step": round(el / k * 1e3, 4), "bytes_per_gpu": bs * nb,
-            "kernel": ctx_path_bs(bs), "roofline": {"achieved": round(alg / (kms * 1e-3) / 1e9, 1),
+            "kernel": ctx.blocks_plan(region.data_ptr(), nb, bs), "roofline": {"achieved": round(alg / (kms * 1e-3) / 1e9, 1),
                                                       "peak": HBM_PEAK_GBS, "unit": "GB/s",
                                                       "frac": round(alg / (kms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                                                       "kernel_ms": round(kms, 4)},
@@ -383,40 +383,6 @@ def cpu_baseline(O, host, bs, gpu_crc):
                        f"server/Makefile:25-26) at 1 and {nthr} threads (static block split)",
              "variants": variants, "threads_used": nthr, "cpus_in_affinity": avail, "cpu": cpu_model(),
              "compiler": info.get("compiler")}, ok)
-
-
-def ctx_path_bs(bs):
-    from priskv_amd import blocks_path
-    return rows_plan_name(bs) if blocks_path(16 << 10, 1, bs) == "rows" else f"crc_{blocks_path(16 << 10, 1, bs)}_kernel"
-
-
-def ctx_path(bs, region):
-    """Kernel the library dispatches to (mirrors plan_for() in crc_gpu.hip)."""
-    from priskv_amd import blocks_path
-    p = blocks_path(region.data_ptr(), 1, bs)
-    return rows_plan_name(bs) if p == "rows" else f"crc_{p}_kernel"
-
-
-def rows_plan_name(bs):
-    pipe = bs in (1024, 4096)
-    if bs == 4096:
-        g, ch = 32, 8
-    elif bs <= 16384 and bs % 4096:
-        g, ch = 16, 4
-    else:
-        r = bs // 1024
-        g, ch = 64, (4 if r % 4 == 0 else (2 if r % 2 == 0 else 1))
-    w = os.environ.get("PRISKV_CRC_XCD_WEIGHTS", "31:29")
-    split = "" if w.replace(" ", "") in ("1:1",) else f",xcd-weighted {w}"
-    fold = ",pipelined-fold" if pipe else ""
-    if bs in (1024, 4096, 8192):
-        fold += ",nibble-table-fold"
-    # progress-priority mode of the plan (kPlans in crc_gpu.hip)
-    mode = 3 if bs == 4096 or (g == 64 and ch == 4 and bs >= 256 << 10) else (1 if ch == 4 or g == 16 else 0)
-    if os.environ.get("PRISKV_CRC_PRIO") == "0":
-        mode = 0
-    prio = f",progress-priority {mode}" if mode else ""
-    return f"crc_rows_kernel<G={g},CH={ch},NBUF=2,nt{fold}{split}{prio}>"
 
 
 def cpu_model():

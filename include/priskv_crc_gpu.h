@@ -181,6 +181,15 @@ int priskv_crc_fill_splitmix_dev(const priskv_crc_ctx *ctx, void *d_dst, uint64_
  * benchmarks; -EINVAL for invalid arguments. */
 int priskv_crc32_blocks_path(const void *d_base, uint64_t nblocks, uint32_t block_size);
 
+/* The kernel plan priskv_crc32_blocks_dev would launch for this batch on
+ * this context, as a NUL-terminated description in buf (at most len bytes),
+ * e.g. "crc_rows_kernel<G=64,CH=4,NBUF=3,nt,pipelined-fold,nibble-fold,
+ * progress-priority 3,xcd-weighted 31:29>".  It reflects the context's
+ * options (PRISKV_CRC_PRIO / _SEGMENT / _XCD_WEIGHTS and the XCD probe).
+ * Benchmarks and diagnostics; -EINVAL for invalid arguments. */
+int priskv_crc32_blocks_plan(const priskv_crc_ctx *ctx, const void *d_base, uint64_t nblocks, uint32_t block_size,
+                             char *buf, uint64_t len);
+
 const char *priskv_crc_version(void);
 
 #if defined(__cplusplus)

@@ -66,6 +66,8 @@ SIGNATURES = [
     ("priskv_crc_fill_splitmix_dev", _C.c_int,
      [_C.c_void_p, _C.c_void_p, _C.c_uint64, _C.c_uint64, _C.c_uint64, _C.c_void_p]),
     ("priskv_crc32_blocks_path", _C.c_int, [_C.c_void_p, _C.c_uint64, _C.c_uint32]),
+    ("priskv_crc32_blocks_plan", _C.c_int,
+     [_C.c_void_p, _C.c_void_p, _C.c_uint64, _C.c_uint32, _C.c_char_p, _C.c_uint64]),
     ("priskv_crc_version", _C.c_char_p, []),
 ]
 
@@ -144,6 +146,15 @@ def _device_args(region, *tensors) -> None:
             raise ValueError("offsets / lengths / out must be contiguous tensors on the region's device")
 
 
+def _host_out(out: Optional[np.ndarray], n: int) -> np.ndarray:
+    """A host result array the C code may write n uint32 entries into."""
+    if out is None:
+        return np.empty(n, dtype=np.uint32)
+    if not isinstance(out, np.ndarray) or out.dtype != np.uint32 or not out.flags.c_contiguous or out.size < n:
+        raise ValueError(f"out must be a C-contiguous uint32 numpy array of >= {n} entries")
+    return out
+
+
 def _stream_ptr(stream) -> Optional[int]:
     if stream is None:
         import torch
@@ -182,6 +193,13 @@ class CrcContext:
     def handle(self) -> ctypes.c_void_p:
         return self._h
 
+    def blocks_plan(self, region_ptr: int, nblocks: int, block_size: int) -> str:
+        """The kernel plan blocks_dev would launch (priskv_crc32_blocks_plan)."""
+        buf = ctypes.create_string_buffer(256)
+        _check(lib().priskv_crc32_blocks_plan(self._h, region_ptr, nblocks, block_size, buf, len(buf)),
+               "priskv_crc32_blocks_plan")
+        return buf.value.decode()
+
     # ---- device-resident
     def blocks_dev(self, region, block_size: int, out=None, stream=None, nblocks: Optional[int] = None):
         """d_out[i] = priskv_crc32(region + i*block_size, block_size); returns an int32 cuda
@@ -197,6 +215,7 @@ class CrcContext:
             out = torch.empty(n, dtype=torch.int32, device=region.device)
         if out.numel() < n or out.element_size() != 4 or not out.is_contiguous():
             raise ValueError("out must be a contiguous 4-byte tensor of >= nblocks entries")
+        _device_args(region, out)
         _check(lib().priskv_crc32_blocks_dev(self._h, region.data_ptr(), n, block_size, out.data_ptr(),
                                              _stream_ptr(stream)), "priskv_crc32_blocks_dev")
         return out
@@ -249,8 +268,7 @@ class CrcContext:
     def blocks_host(self, region: np.ndarray, block_size: int, out: Optional[np.ndarray] = None) -> np.ndarray:
         region = np.ascontiguousarray(region).view(np.uint8).reshape(-1)
         n = region.size // block_size
-        if out is None:
-            out = np.empty(n, dtype=np.uint32)
+        out = _host_out(out, n)
         _check(lib().priskv_crc32_blocks_host(self._h, region.ctypes.data, n, block_size, out.ctypes.data),
                "priskv_crc32_blocks_host")
         return out
@@ -263,8 +281,7 @@ def _ranges_host(self, region: np.ndarray, offsets, lengths, out: Optional[np.nd
     lens = np.ascontiguousarray(lengths, dtype=np.uint32)
     if offs.shape != lens.shape:
         raise ValueError("offsets and lengths must have the same length")
-    if out is None:
-        out = np.empty(offs.size, dtype=np.uint32)
+    out = _host_out(out, offs.size)
     _check(lib().priskv_crc32_ranges_host(self._h, region.ctypes.data, region.size, offs.ctypes.data,
                                           lens.ctypes.data, offs.size, out.ctypes.data),
            "priskv_crc32_ranges_host")
@@ -283,8 +300,7 @@ def blocks_host_multi(ctxs, region: np.ndarray, block_size: int, out: Optional[n
     """Host-resident blocks split across several contexts (one GPU each)."""
     region = np.ascontiguousarray(region).view(np.uint8).reshape(-1)
     n = region.size // block_size
-    if out is None:
-        out = np.empty(n, dtype=np.uint32)
+    out = _host_out(out, n)
     _check(lib().priskv_crc32_blocks_host_multi(_ctx_array(ctxs), len(ctxs), region.ctypes.data, n, block_size,
                                                 out.ctypes.data), "priskv_crc32_blocks_host_multi")
     return out
@@ -295,8 +311,9 @@ def ranges_host_multi(ctxs, region: np.ndarray, offsets, lengths, out: Optional[
     region = np.ascontiguousarray(region).view(np.uint8).reshape(-1)
     offs = np.ascontiguousarray(offsets, dtype=np.uint64)
     lens = np.ascontiguousarray(lengths, dtype=np.uint32)
-    if out is None:
-        out = np.empty(offs.size, dtype=np.uint32)
+    if offs.shape != lens.shape:
+        raise ValueError("offsets and lengths must have the same length")
+    out = _host_out(out, offs.size)
     _check(lib().priskv_crc32_ranges_host_multi(_ctx_array(ctxs), len(ctxs), region.ctypes.data, region.size,
                                                 offs.ctypes.data, lens.ctypes.data, offs.size, out.ctypes.data),
            "priskv_crc32_ranges_host_multi")

@@ -15,6 +15,15 @@
 // atomic count of queued values; the worker is woken on the empty -> non-empty
 // transition and when the count reaches max_batch.  Callbacks for one thread's
 // submissions come in that thread's submission order.
+//
+// Flush is by gather generation, not by counts: the worker numbers each pass
+// over the shards (gen_started, under mu) and publishes the number of the last
+// pass whose callbacks are done (gen_done).  A value whose submit returned
+// before flush() read gen_started is in a shard before pass gen_started + 1
+// visits that shard, so it is called back by the time gen_done reaches
+// gen_started + 1.  (Counting values instead is racy: a pass visits the shards
+// one by one and can pick up a later value from one shard while an earlier
+// value in a shard it already visited waits for the next pass.)
 #include <errno.h>
 #include <stdint.h>
 
@@ -62,13 +71,15 @@ struct priskv_crc_batch {
 
     Shard shards[kShards];
     std::atomic<uint64_t> queued{0};     // values in the shards
-    std::atomic<uint64_t> submitted{0};  // accepted by submit[v]
     std::atomic<int64_t> oldest_ns{0};   // when the queue last became non-empty
-    std::mutex mu;                       // worker sleep / flush / backpressure / stop
+    std::mutex mu;                       // worker sleep / flush / backpressure
     std::condition_variable cv_work, cv_room, cv_done;
-    uint64_t completed = 0;              // guarded by mu
-    int flushers = 0;                    // guarded by mu: no deadline waits while > 0
-    bool stop = false;                   // guarded by mu
+    uint64_t gen_started = 0;            // guarded by mu: passes over the shards begun
+    uint64_t gen_done = 0;               // guarded by mu: passes whose callbacks are done
+    uint64_t flush_target = 0;           // guarded by mu: a flusher waits for gen_done >= this
+    // set by destroy, which by contract runs with no submit in flight; read
+    // by submitters without the lock (it only turns late misuse into -EINVAL)
+    std::atomic<bool> stop{false};
     std::thread worker;
 
     void wake()
@@ -86,7 +97,7 @@ struct priskv_crc_batch {
             wake();
         if (prev + k > kBacklogBatches * max_batch) {
             std::unique_lock<std::mutex> lk(mu);
-            cv_room.wait(lk, [this] { return queued.load() <= kBacklogBatches * max_batch || stop; });
+            cv_room.wait(lk, [this] { return queued.load() <= kBacklogBatches * max_batch || stop.load(); });
         }
     }
 
@@ -95,14 +106,15 @@ struct priskv_crc_batch {
         std::vector<uint64_t> off, cookie;
         std::vector<uint32_t> len, crc;
         for (;;) {
+            uint64_t gen;
             {
                 std::unique_lock<std::mutex> lk(mu);
                 for (;;) {
                     const uint64_t q = queued.load();
-                    if (q >= max_batch || ((stop || flushers) && q))
-                        break;
+                    if (q >= max_batch || (stop.load() && q) || gen_done < flush_target)
+                        break; // a flusher's pass runs even when nothing is queued
                     if (q == 0) {
-                        if (stop)
+                        if (stop.load())
                             return;
                         cv_work.wait(lk);
                         continue;
@@ -112,6 +124,7 @@ struct priskv_crc_batch {
                     if (cv_work.wait_until(lk, deadline) == std::cv_status::timeout)
                         break;
                 }
+                gen = ++gen_started;
             }
             off.clear();
             len.clear();
@@ -141,7 +154,7 @@ struct priskv_crc_batch {
             }
             {
                 std::lock_guard<std::mutex> lk(mu);
-                completed += off.size();
+                gen_done = gen;
             }
             cv_done.notify_all();
         }
@@ -199,11 +212,8 @@ PRV_API int priskv_crc_batch_submitv(priskv_crc_batch *b, uint64_t n, const uint
             return -EINVAL;
     if (n == 0)
         return 0;
-    {
-        std::lock_guard<std::mutex> lk(b->mu);
-        if (b->stop)
-            return -EINVAL;
-    }
+    if (b->stop.load(std::memory_order_relaxed))
+        return -EINVAL;
     // count first, then publish: `queued` never drops below the values in the
     // shards, so the worker's subtraction of what it gathered cannot wrap
     const uint64_t prev = b->queued.fetch_add(n);
@@ -214,7 +224,6 @@ PRV_API int priskv_crc_batch_submitv(priskv_crc_batch *b, uint64_t n, const uint
         s.len.insert(s.len.end(), valuelens, valuelens + n);
         s.cookie.insert(s.cookie.end(), cookies, cookies + n);
     }
-    b->submitted.fetch_add(n);
     b->queued_more(prev, n);
     return 0;
 }
@@ -229,11 +238,13 @@ PRV_API int priskv_crc_batch_flush(priskv_crc_batch *b)
     if (!b)
         return -EINVAL;
     std::unique_lock<std::mutex> lk(b->mu);
-    const uint64_t target = b->submitted.load();
-    b->flushers++; // the worker stops waiting for deadlines while we wait
+    // the first pass to begin after this point sees every value published
+    // before it (see the file comment)
+    const uint64_t target = b->gen_started + 1;
+    if (b->flush_target < target)
+        b->flush_target = target;
     b->cv_work.notify_one();
-    b->cv_done.wait(lk, [b, target] { return b->completed >= target; });
-    b->flushers--;
+    b->cv_done.wait(lk, [b, target] { return b->gen_done >= target; });
     return 0;
 }
 
@@ -243,7 +254,7 @@ PRV_API void priskv_crc_batch_destroy(priskv_crc_batch *b)
         return;
     {
         std::lock_guard<std::mutex> lk(b->mu);
-        b->stop = true; // the worker drains the queue, then exits
+        b->stop.store(true); // the worker drains the queue, then exits
         b->cv_work.notify_one();
         b->cv_room.notify_all();
     }

@@ -37,6 +37,8 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <vector>
+
 #include "../../include/priskv_crc_gpu.h"
 #include "crc_internal.h"
 
@@ -70,6 +72,7 @@ struct priskv_crc_ctx {
     int prio;                  // rows kernel progress priority (PRISKV_CRC_PRIO=0: off)
     int balance;               // byte-balanced extents split (PRISKV_CRC_BALANCE=0: off)
     uint64_t seg_max_extents;  // device-resident lengths: segment calls of at most this many extents
+    int xcd_rr;                // the XCD probe found workgroup b on XCD b % 8 (weights apply)
     uint32_t *d_lds_image[3];  // 64 KiB each: set B gap for G = 64, 32, 16
     uint32_t *d_fold;          // kFoldSets x 2048 words, set j for G = 1 << j
     uint32_t *d_nibrep[7];     // nibble fold tables for G = 1 << j (j >= 1), 8 x 16 x max(G, 32) words
@@ -245,7 +248,7 @@ int launch_generic(const priskv_crc_ctx *ctx, const uint8_t *base, uint64_t n, u
     return herr(hipGetLastError());
 }
 
-constexpr int kNbuf = 2;  // register pipeline depth (chunks)
+constexpr int kNbuf = 2;  // register pipeline depth (chunks) of the extents kernel
 constexpr int kAux = 2;   // cache policy of the streaming loads: nt
 constexpr int kExtRows = 2; // rows per chunk of the extents kernel (tools/ranges_explore)
 // extents kernel: nibble fold + row apply (bit 0), masks only where needed
@@ -341,7 +344,7 @@ int launch_extents(const priskv_crc_ctx *ctx, const uint8_t *base, uint64_t n, c
 // (NBUF = 2) and cache policy (nt) are fixed.
 
 enum PlanId {
-    PLAN_G32_CH8_PIPE, // 4 KiB: one chunk == one 2-block group, fold pipelined, nibble-table fold
+    PLAN_4K,           // 4 KiB: G64, CH4, 3 chunks in flight, one chunk == one block, fold pipelined, nibble fold
     PLAN_G64_CH4_NIB,  // 8 KiB: G64 with the nibble fold (every 2 chunks)
     PLAN_G16_CH4_PIPE, // 1 KiB (same two folds)
     PLAN_G16_CH4,      // other multiples of 1 KiB up to 16 KiB
@@ -353,7 +356,7 @@ enum PlanId {
 };
 static_assert(NPLANS <= 8, "priskv_crc_ctx per-plan arrays");
 struct Plan {
-    int G, CH, opt, wg_per_cu;
+    int G, CH, NBUF, opt, wg_per_cu;
     uint32_t we, wo; // even:odd XCD weights of the static split
 };
 // opt = crc_rows_kernel OPT bits: 2 = pipelined fold, 32 = nibble-table fold,
@@ -362,16 +365,21 @@ struct Plan {
 // (profiles/r01/prio/occupancy_*.log).
 // Weights: swept per plan (profiles/r01/explore_*_xw*.log, bench_xw_ab.jsonl);
 // 31:29 is best or within noise for every plan in bench.py's sustained loop.
+// 4 KiB: G64 / CH4 / NBUF3 replaced G32 / CH8 / NBUF2 in round 2 -- finer
+// chunks with three in flight keep more bytes in flight while a wave hashes;
+// +1.4-2.1 % in the explorer on two boxes, same process, bit-identical
+// (profiles/r02/explore_4k_*.log).  NBUF3 loses 1-3 % at 8 KiB-1 MiB
+// (profiles/r02/explore_{8k,64k,1m}_nbuf*.log), so those keep NBUF2.
 constexpr int kPrio1 = 1 << 8, kPrio3 = 3 << 8;
 constexpr Plan kPlans[NPLANS] = {
-    {32, 8, 2 | 32 | kPrio3, 1, 31, 29}, {64, 4, 32 | kPrio1, 1, 31, 29}, {16, 4, 2 | 32 | kPrio1, 1, 31, 29},
-    {16, 4, kPrio1, 1, 31, 29},          {64, 4, kPrio1, 1, 31, 29},      {64, 4, kPrio3, 1, 31, 29},
-    {64, 2, 0, 1, 31, 29},               {64, 1, 0, 1, 31, 29}};
+    {64, 4, 3, 2 | 32 | kPrio3, 1, 31, 29}, {64, 4, 2, 32 | kPrio1, 1, 31, 29}, {16, 4, 2, 2 | 32 | kPrio1, 1, 31, 29},
+    {16, 4, 2, kPrio1, 1, 31, 29},          {64, 4, 2, kPrio1, 1, 31, 29},      {64, 4, 2, kPrio3, 1, 31, 29},
+    {64, 2, 2, 0, 1, 31, 29},               {64, 1, 2, 0, 1, 31, 29}};
 
 int plan_for(uint32_t bs)
 {
     if (bs == 4096)
-        return PLAN_G32_CH8_PIPE;
+        return PLAN_4K;
     if (bs == 8192)
         return PLAN_G64_CH4_NIB;
     if (bs == 1024)
@@ -384,10 +392,10 @@ int plan_for(uint32_t bs)
     return R % 2 == 0 ? PLAN_G64_CH2 : PLAN_G64_CH1;
 }
 
-template <int G, int CH, int OPT>
+template <int G, int CH, int NB, int OPT>
 const void *plan_kernel()
 {
-    return reinterpret_cast<const void *>(&crc_rows_kernel<G, CH, kNbuf, kAux, OPT>);
+    return reinterpret_cast<const void *>(&crc_rows_kernel<G, CH, NB, kAux, OPT>);
 }
 
 // prio = false: the plan's kernel without progress priority (PRISKV_CRC_PRIO=0)
@@ -395,13 +403,13 @@ template <int P>
 const void *plan_kernel_p(bool prio)
 {
     constexpr Plan Q = kPlans[P];
-    return prio ? plan_kernel<Q.G, Q.CH, Q.opt>() : plan_kernel<Q.G, Q.CH, (Q.opt & ~(3 << 8))>();
+    return prio ? plan_kernel<Q.G, Q.CH, Q.NBUF, Q.opt>() : plan_kernel<Q.G, Q.CH, Q.NBUF, (Q.opt & ~(3 << 8))>();
 }
 
 const void *plan_fn(int p, bool prio)
 {
     switch (p) {
-    case PLAN_G32_CH8_PIPE: return plan_kernel_p<PLAN_G32_CH8_PIPE>(prio);
+    case PLAN_4K: return plan_kernel_p<PLAN_4K>(prio);
     case PLAN_G64_CH4_NIB: return plan_kernel_p<PLAN_G64_CH4_NIB>(prio);
     case PLAN_G16_CH4_PIPE: return plan_kernel_p<PLAN_G16_CH4_PIPE>(prio);
     case PLAN_G16_CH4: return plan_kernel_p<PLAN_G16_CH4>(prio);
@@ -648,12 +656,14 @@ int launch_blocks(const priskv_crc_ctx *ctx, const uint8_t *base, uint64_t nbloc
 // XCD weights of the rows-kernel split: on a multi-XCD device
 // (workgroups dispatched round-robin over 8 XCDs) waves on odd XCDs finish
 // later under an equal split on every MI355X measured, so even-XCD waves take
-// more parts (kPlans[p].we : wo).  PRISKV_CRC_XCD_WEIGHTS="we:wo" overrides
-// every plan ("1:1" = equal split).
-uint32_t xcd_weights(int num_cus, int p)
+// more parts (kPlans[p].we : wo).  Only when the context's probe saw
+// workgroup b on XCD b % 8 (xcd_rr); otherwise -- another partition mode, a
+// different XCD count -- the split is equal.  PRISKV_CRC_XCD_WEIGHTS="we:wo"
+// overrides every plan ("1:1" = equal split) and applies regardless.
+uint32_t xcd_weights(int xcd_rr, int p)
 {
     uint32_t we = kPlans[p].we, wo = kPlans[p].wo;
-    if (num_cus < 64 || num_cus % 8) // one XCD (or a partition mode): nothing to balance
+    if (!xcd_rr)
         we = wo = 1;
     if (const char *e = getenv("PRISKV_CRC_XCD_WEIGHTS")) {
         unsigned a = 0, b = 0;
@@ -663,6 +673,37 @@ uint32_t xcd_weights(int num_cus, int p)
         }
     }
     return we == wo ? 0u : ((we << 16) | wo);
+}
+
+// Does workgroup b of a launch run on XCD b % 8 (8 XCDs, round-robin)?
+// One launch of 64 single-wave workgroups on the context's stream.
+// PRISKV_CRC_XCD_PROBE=0 forces "no" (tests of the fallback).
+int xcd_probe(priskv_crc_ctx *c, int *rr)
+{
+    *rr = 0;
+    if (const char *e = getenv("PRISKV_CRC_XCD_PROBE"))
+        if (!strcmp(e, "0"))
+            return 0;
+    if (c->num_cus < 64 || c->num_cus % 8)
+        return 0;
+    constexpr int kProbeWgs = 64;
+    uint32_t *d = nullptr;
+    uint32_t h[kProbeWgs];
+    int rc = herr(hipMalloc((void **)&d, sizeof(h)));
+    if (rc)
+        return rc;
+    hipLaunchKernelGGL(crc_xcd_probe_kernel, dim3(kProbeWgs), dim3(64), 0, c->aux, d);
+    if (!(rc = herr(hipGetLastError())) &&
+        !(rc = herr(hipMemcpyAsync(h, d, sizeof(h), hipMemcpyDeviceToHost, c->aux))))
+        rc = herr(hipStreamSynchronize(c->aux));
+    (void)hipFree(d);
+    if (rc)
+        return rc;
+    int ok = 1;
+    for (int b = 0; b < kProbeWgs; b++)
+        ok &= h[b] == (uint32_t)(b % 8);
+    *rr = ok;
+    return 0;
 }
 
 // resident workgroups per CU of every plan: the plan's choice, capped by
@@ -690,6 +731,40 @@ int priskv_crc32_blocks_path(const void *d_base, uint64_t nblocks, uint32_t bloc
     if (block_size == 0 || (nblocks && !d_base))
         return -EINVAL;
     return choose_path(d_base, block_size);
+}
+
+int priskv_crc32_blocks_plan(const priskv_crc_ctx *ctx, const void *d_base, uint64_t nblocks, uint32_t block_size,
+                             char *buf, uint64_t len)
+{
+    if (!ctx || block_size == 0 || !buf || len == 0)
+        return -EINVAL;
+    const int path = choose_path(d_base, block_size);
+    int w = 0;
+    if (path == PATH_ROWS) {
+        const uint32_t S = segments_for(ctx, nblocks, block_size);
+        const uint32_t bs = block_size / S;
+        const int p = plan_for(bs);
+        const Plan &P = kPlans[p];
+        const uint32_t xw = ctx->plan_xw[p];
+        const int mode = ctx->prio ? (P.opt >> 8) & 3 : 0;
+        w = snprintf(buf, len, "crc_rows_kernel<G=%d,CH=%d,NBUF=%d,nt%s%s", P.G, P.CH, P.NBUF,
+                     (P.opt & 2) ? ",pipelined-fold" : "", (P.opt & 32) ? ",nibble-fold" : "");
+        if (w >= 0 && (uint64_t)w < len && mode)
+            w += snprintf(buf + w, len - w, ",progress-priority %d", mode);
+        if (w >= 0 && (uint64_t)w < len && xw)
+            w += snprintf(buf + w, len - w, ",xcd-weighted %u:%u", xw >> 16, xw & 0xFFFF);
+        if (w >= 0 && (uint64_t)w < len)
+            w += snprintf(buf + w, len - w, ">%s", S > 1 ? " x segments + crc_combine_segments_kernel" : "");
+        if (w >= 0 && (uint64_t)w < len && S > 1)
+            w += snprintf(buf + w, len - w, " (%u segments of %u B per block)", S, bs);
+    } else if (path == PATH_SMALL) {
+        w = snprintf(buf, len, "crc_small_kernel<G=%u>", block_size / 16);
+    } else if (path == PATH_EXTENTS) {
+        w = snprintf(buf, len, "crc_ranges_kernel (extents)");
+    } else {
+        w = snprintf(buf, len, "crc_generic_kernel");
+    }
+    return w < 0 ? -EIO : 0;
 }
 
 int priskv_crc_ctx_create(int device, priskv_crc_ctx **out)
@@ -720,8 +795,6 @@ int priskv_crc_ctx_create(int device, priskv_crc_ctx **out)
     if ((rc = herr(hipDeviceGetAttribute(&c->num_cus, hipDeviceAttributeMultiprocessorCount, device))))
         goto fail;
     c->max_wgs = 2 * c->num_cus;
-    for (int p = 0; p < NPLANS; p++)
-        c->plan_xw[p] = xcd_weights(c->num_cus, p);
     {
         const char *e = getenv("PRISKV_CRC_SEGMENT");
         c->segment = !(e && !strcmp(e, "0"));
@@ -776,6 +849,10 @@ int priskv_crc_ctx_create(int device, priskv_crc_ctx **out)
         goto fail;
     if ((rc = herr(hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking))))
         goto fail;
+    if ((rc = xcd_probe(c, &c->xcd_rr)))
+        goto fail;
+    for (int p = 0; p < NPLANS; p++)
+        c->plan_xw[p] = xcd_weights(c->xcd_rr, p);
     {
         int ev_ok = 1; // without the events every call keeps its own alloc/free
         for (int i = 0; i < NPOOL; i++)
@@ -946,6 +1023,99 @@ int priskv_crc_host_unregister(void *h_base)
     return herr(hipHostUnregister(h_base));
 }
 
+namespace {
+// Is [h, h + len) one contiguous device-visible mapping (registered or
+// pinned)?  Both ends are looked up: a registration that ends inside the
+// range would otherwise pass as a mapping of all of it.
+bool host_mapped(const void *h, uint64_t len, void **dptr)
+{
+    void *d0 = nullptr, *d1 = nullptr;
+    const uint8_t *last = (const uint8_t *)h + len - 1;
+    const bool ok = hipHostGetDevicePointer(&d0, const_cast<void *>(h), 0) == hipSuccess && d0 &&
+                    hipHostGetDevicePointer(&d1, const_cast<uint8_t *>(last), 0) == hipSuccess && d1 &&
+                    (uint8_t *)d1 - (uint8_t *)d0 == (ptrdiff_t)(len - 1);
+    (void)hipGetLastError();
+    *dptr = ok ? d0 : nullptr;
+    return ok;
+}
+
+// Registrations this library makes on the caller's behalf (the zero-copy
+// scrub of a region the caller did not register).  One process-wide registry
+// keyed by base: concurrent calls over the same region -- several GPUs
+// scrubbing one memfile, the batcher beside a scrub -- share one
+// registration, and the last user unregisters it.  Check, register and
+// refcount happen under one lock, so no caller can see another's temporary
+// mapping disappear while its kernel still reads it.
+struct TempReg {
+    const void *base;
+    uint64_t len;
+    int refs;
+};
+pthread_mutex_t g_reg_lock = PTHREAD_MUTEX_INITIALIZER;
+std::vector<TempReg> g_regs;
+
+// *dptr = device view of [base, base + len); *held = a registry reference
+// was taken (release it with reg_release)
+int reg_acquire(const void *base, uint64_t len, void **dptr, bool *held)
+{
+    *held = false;
+    pthread_mutex_lock(&g_reg_lock);
+    int rc = 0;
+    for (TempReg &r : g_regs) {
+        if (r.base != base)
+            continue;
+        if (r.len < len) {
+            rc = -EBUSY; // a shorter temporary mapping of the same base is in use
+        } else {
+            r.refs++;
+            *held = true;
+            if (!host_mapped(base, len, dptr))
+                rc = -EIO;
+        }
+        if (rc && *held) {
+            r.refs--;
+            *held = false;
+        }
+        pthread_mutex_unlock(&g_reg_lock);
+        return rc;
+    }
+    if (host_mapped(base, len, dptr)) { // the caller's own registration / pinned memory
+        pthread_mutex_unlock(&g_reg_lock);
+        return 0;
+    }
+    rc = herr(hipHostRegister(const_cast<void *>(base), len, hipHostRegisterPortable | hipHostRegisterMapped));
+    if (!rc && !host_mapped(base, len, dptr)) {
+        (void)hipHostUnregister(const_cast<void *>(base));
+        rc = -EIO;
+    }
+    if (!rc) {
+        try {
+            g_regs.push_back(TempReg{base, len, 1});
+            *held = true;
+        } catch (...) {
+            (void)hipHostUnregister(const_cast<void *>(base));
+            rc = -ENOMEM;
+        }
+    }
+    pthread_mutex_unlock(&g_reg_lock);
+    return rc;
+}
+
+void reg_release(const void *base)
+{
+    pthread_mutex_lock(&g_reg_lock);
+    for (size_t i = 0; i < g_regs.size(); i++) {
+        if (g_regs[i].base != base)
+            continue;
+        if (--g_regs[i].refs == 0) {
+            (void)hipHostUnregister(const_cast<void *>(base));
+            g_regs.erase(g_regs.begin() + (ptrdiff_t)i);
+        }
+        break;
+    }
+    pthread_mutex_unlock(&g_reg_lock);
+}
+} // namespace
 
 int priskv_crc32_ranges_host(priskv_crc_ctx *ctx, const void *h_base, uint64_t region_bytes,
                              const uint64_t *h_offsets, const uint32_t *h_lengths, uint64_t n, uint32_t *h_out)
@@ -965,21 +1135,12 @@ int priskv_crc32_ranges_host(priskv_crc_ctx *ctx, const void *h_base, uint64_t r
     DevGuard g(ctx->device);
     if (!g.ok)
         return -ENODEV;
-    // device view of the host mapping (zero-copy): registered/pinned memory
-    // has one; otherwise register it for this call
+    // device view of the host mapping (zero-copy): the caller's registration
+    // or pinned memory, else a shared temporary registration (reg_acquire)
     void *dptr = nullptr;
-    bool temp_reg = false;
-    if (hipHostGetDevicePointer(&dptr, const_cast<void *>(h_base), 0) != hipSuccess || !dptr) {
-        (void)hipGetLastError();
-        if (int rc = herr(hipHostRegister(const_cast<void *>(h_base), region_bytes,
-                                          hipHostRegisterPortable | hipHostRegisterMapped)))
-            return rc;
-        temp_reg = true;
-        if (int rc = herr(hipHostGetDevicePointer(&dptr, const_cast<void *>(h_base), 0))) {
-            (void)hipHostUnregister(const_cast<void *>(h_base));
-            return rc;
-        }
-    }
+    bool held = false;
+    if (int rc = reg_acquire(h_base, region_bytes, &dptr, &held))
+        return rc;
     pthread_mutex_lock(&ctx->lock);
     int rc = 0;
     const size_t need = (size_t)n * (8 + 4 + 4);
@@ -1003,8 +1164,8 @@ int priskv_crc32_ranges_host(priskv_crc_ctx *ctx, const void *h_base, uint64_t r
             (void)hipStreamSynchronize(ctx->aux);
     }
     pthread_mutex_unlock(&ctx->lock);
-    if (temp_reg)
-        (void)hipHostUnregister(const_cast<void *>(h_base));
+    if (held)
+        reg_release(h_base);
     return rc;
 }
 
@@ -1118,20 +1279,15 @@ int priskv_crc32_ranges_host_multi(priskv_crc_ctx *const *ctxs, int nctx, const 
     p.lens = h_lengths;
     p.out = h_out;
     p.ranges = true;
-    // register the mapping once for all devices (the per-shard calls would
-    // otherwise race to register the same range)
+    // one shared registration for all devices (the per-shard calls then find
+    // it in the registry instead of each registering the range)
     void *probe = nullptr;
-    bool temp_reg = false;
-    if (hipHostGetDevicePointer(&probe, const_cast<void *>(h_base), 0) != hipSuccess || !probe) {
-        (void)hipGetLastError();
-        if (int rc = herr(hipHostRegister(const_cast<void *>(h_base), region_bytes,
-                                          hipHostRegisterPortable | hipHostRegisterMapped)))
-            return rc;
-        temp_reg = true;
-    }
+    bool held = false;
+    if (int rc = reg_acquire(h_base, region_bytes, &probe, &held))
+        return rc;
     const int rc = run_multi(ctxs, nctx, p, n);
-    if (temp_reg)
-        (void)hipHostUnregister(const_cast<void *>(h_base));
+    if (held)
+        reg_release(h_base);
     return rc;
 }
 
@@ -1245,13 +1401,10 @@ int priskv_crc32_blocks_host(priskv_crc_ctx *ctx, const void *h_base, uint64_t n
         return rc;
     }
     // pinned / registered input is DMA'd directly; pageable input bounces
-    bool pinned = false;
-    {
-        hipPointerAttribute_t attr;
-        if (hipPointerGetAttributes(&attr, h_base) == hipSuccess && attr.type == hipMemoryTypeHost)
-            pinned = true;
-        (void)hipGetLastError();
-    }
+    // (the whole batch, both ends: a registration that stops short of the
+    // last block would have the DMA read unpinned pages)
+    void *dview = nullptr;
+    const bool pinned = host_mapped(h_base, nblocks * (uint64_t)block_size, &dview);
     const uint64_t per = ctx->chunk_bytes / block_size;
     const uint64_t nchunks = (nblocks + per - 1) / per;
     uint64_t pending_first[NSTREAM], pending_n[NSTREAM];

@@ -933,3 +933,155 @@ def test_tib_config_per_gpu_shard(torch_cuda, ctx):
     assert np.array_equal(cx, a ^ np.uint32(crc_c))
     del t, tv, c64
     torch.cuda.empty_cache()
+
+
+def _ctx_env(**env):
+    """A context created with the given PRISKV_CRC_* environment (read at creation)."""
+    import os
+    from priskv_amd import CrcContext
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update({k: str(v) for k, v in env.items()})
+    try:
+        return CrcContext(0)
+    finally:
+        for k, v in old.items():
+            if v is None:
+                del os.environ[k]
+            else:
+                os.environ[k] = v
+
+
+@pytest.mark.parametrize("bs", [4096, 8192, 65536, 1 << 20])
+def test_xcd_weights_and_probe_fallback(torch_cuda, ctx, bs):
+    """The XCD-weighted split (workgroup b assumed on XCD b % 8, checked by a
+    probe at context creation), an override, equal shares, and the probe's
+    forced fallback give the oracle's CRCs; the plan string says which split
+    each context uses."""
+    torch = torch_cuda
+    nb = max(64, (96 << 20) // bs) + 1
+    t = _region(torch, ctx, bs * nb, SEED ^ bs ^ 0x3C, nb)
+    want = O.crc32_blocks(t[: bs * nb].cpu().numpy(), bs, nthreads=8)
+    ctxs = {"default": ctx, "1:1": _ctx_env(PRISKV_CRC_XCD_WEIGHTS="1:1"),
+            "17:13": _ctx_env(PRISKV_CRC_XCD_WEIGHTS="17:13"), "fallback": _ctx_env(PRISKV_CRC_XCD_PROBE="0")}
+    plans = {}
+    for name, c in ctxs.items():
+        got = _u32(c.blocks_dev(t, bs, nblocks=nb))
+        torch.cuda.synchronize()
+        assert np.array_equal(got, want), (name, np.nonzero(got != want)[0][:8])
+        plans[name] = c.blocks_plan(t.data_ptr(), nb, bs)
+    assert "xcd-weighted" not in plans["1:1"] and "xcd-weighted" not in plans["fallback"], plans
+    assert "xcd-weighted 17:13" in plans["17:13"], plans
+    # MI355X dispatches workgroups round-robin over its 8 XCDs: the probe agrees
+    assert "xcd-weighted 31:29" in plans["default"], plans
+    for name in ("1:1", "17:13", "fallback"):
+        ctxs[name].close()
+
+
+def test_blocks_plan_strings(torch_cuda, ctx):
+    """priskv_crc32_blocks_plan names the kernel blocks_dev launches."""
+    base = 1 << 20  # any 16-B aligned address: the plan does not dereference it
+    assert ctx.blocks_plan(base, 1 << 20, 4096).startswith("crc_rows_kernel<G=64,CH=4,NBUF=3,nt,pipelined-fold,"
+                                                             "nibble-fold,progress-priority 3")
+    assert ctx.blocks_plan(base, 1 << 16, 65536).startswith("crc_rows_kernel<G=64,CH=4,NBUF=2,nt,progress-priority 1")
+    assert "segments" in ctx.blocks_plan(base, 1, 1 << 20)
+    assert ctx.blocks_plan(base, 100, 256) == "crc_small_kernel<G=16>"
+    assert ctx.blocks_plan(base + 1, 100, 4096) == "crc_ranges_kernel (extents)"
+    assert ctx.blocks_plan(base, 100, 100) == "crc_generic_kernel"
+
+
+def test_ranges_host_concurrent_temporary_registration(torch_cuda):
+    """Two threads, two contexts, one region nobody registered: every call
+    registers it temporarily through the library's shared registry, so one
+    caller's unregister can never pull the mapping from under the other's
+    kernel, and concurrent registrations never fail with -EEXIST.  The
+    region is left unregistered afterwards."""
+    import threading
+    from priskv_amd import CrcContext, host_register, host_unregister
+    region = O.fill_splitmix(32 << 20, SEED, 41)
+    rng = np.random.default_rng(41)
+    jobs = []
+    for _ in range(2 * 12):
+        lens = rng.integers(0, 300000, 400).astype(np.uint32)
+        offs = np.array([rng.integers(0, region.size - int(ln)) for ln in lens], dtype=np.uint64)
+        jobs.append((offs, lens, O.crc32_ranges(region, offs, lens)))
+    ctxs = [CrcContext(0), CrcContext(0)]
+    errors = []
+
+    def worker(t):
+        try:
+            for j in range(t, len(jobs), 2):
+                offs, lens, want = jobs[j]
+                got = ctxs[t].ranges_host(region, offs, lens)
+                if not np.array_equal(got, want):
+                    errors.append((t, j, "mismatch"))
+        except Exception as e:  # noqa: BLE001 -- reported below
+            errors.append((t, repr(e)))
+
+    th = [threading.Thread(target=worker, args=(t,)) for t in range(2)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    for c in ctxs:
+        c.close()
+    assert not errors, errors[:4]
+    host_register(region)  # would raise EEXIST if a temporary registration had leaked
+    host_unregister(region)
+
+
+def test_batcher_flush_while_others_submit(torch_cuda, ctx):
+    """flush() returns only after every value its thread submitted before it
+    has been called back, while other threads keep submitting (the gather
+    generation rule of crc_batch.cpp)."""
+    import threading
+    from priskv_amd import CrcBatcher
+    region = O.fill_splitmix(16 << 20, SEED, 43)
+    rng = np.random.default_rng(43)
+    k = 4000
+    lens = rng.integers(0, 9000, k).astype(np.uint32)
+    offs = np.array([rng.integers(0, region.size - int(ln)) for ln in lens], dtype=np.uint64)
+    want = O.crc32_ranges(region, offs, lens)
+    got, lock, errors = {}, threading.Lock(), []
+
+    def cb(cookie, crc, status):
+        with lock:
+            got[cookie] = (crc, status)
+
+    with CrcBatcher(ctx, region, cb, max_batch=256, max_delay_us=5000) as b:
+        def worker(t):
+            mine = []
+            for c in range(t * 1000, (t + 1) * 1000, 25):
+                idx = np.arange(c, c + 25)
+                b.submitv(offs[idx], lens[idx], idx)
+                mine.extend(idx.tolist())
+                if (c // 25) % 4 == t % 4:  # flush now and then, others keep submitting
+                    b.flush()
+                    with lock:
+                        missing = [i for i in mine if i not in got]
+                    if missing:
+                        errors.append((t, len(missing)))
+        th = [threading.Thread(target=worker, args=(t,)) for t in range(4)]
+        for x in th:
+            x.start()
+        for x in th:
+            x.join()
+        b.flush()
+    assert not errors, errors[:4]
+    assert len(got) == k and all(got[i] == (int(want[i]), 0) for i in range(k))
+
+
+def test_blocks_host_partially_registered(torch_cuda, ctx):
+    """A registration that covers only the first half of the batch: the
+    streamed path must not DMA the unregistered half as if it were pinned
+    (it takes the bounce path) -- same CRCs as the oracle."""
+    from priskv_amd import host_register, host_unregister
+    bs = 4096
+    nb = (96 << 20) // bs
+    host = O.fill_splitmix(bs * nb, SEED, 47)
+    half = host[: (nb // 2) * bs]
+    host_register(half)
+    try:
+        got = ctx.blocks_host(host, bs)
+    finally:
+        host_unregister(half)
+    assert np.array_equal(got, O.crc32_blocks(host, bs, nthreads=8))

@@ -252,3 +252,15 @@ def test_library_is_not_stale():
     for lib, srcs in deps.items():
         newest = max(os.path.getmtime(p) for p in srcs)
         assert os.path.getmtime(os.path.join(LIBDIR, lib)) >= newest, f"{lib} older than its sources: run make"
+
+
+def test_host_out_arrays_are_checked():
+    """The host paths write n uint32 entries into a caller-supplied `out`:
+    a short, wrong-dtype or strided array is refused before any C call."""
+    from priskv_amd.crc import _host_out
+    assert _host_out(None, 5).dtype == np.uint32
+    ok = np.empty(8, np.uint32)
+    assert _host_out(ok, 8) is ok
+    for bad in (np.empty(4, np.uint32), np.empty(8, np.int64), np.empty(16, np.uint32)[::2], [0] * 8):
+        with pytest.raises(ValueError):
+            _host_out(bad, 8)

@@ -4,7 +4,8 @@
 // and times, interleaved round-robin in ONE process (CDNA guide §5.4 rule 24):
 //   * read-only roofs with the hot kernel's exact access pattern and with a
 //     plain grid-stride stream (what HBM gives this pattern with no hashing);
-//   * crc_rows_kernel variants: prefetch depth (NBUF), cache policy (AUX),
+//   * crc_rows_x_kernel variants (tools/crc_rows_explore.inc: the product
+//     rows kernel plus measurement options): prefetch depth (NBUF), cache policy (AUX),
 //     block assignment (contiguous per wave vs cyclic), workgroups per CU;
 // checking every CRC variant bit-exactly against the first one.
 // Usage: crc_explore [block_size] [nblocks] [rounds]
@@ -22,14 +23,16 @@
 
 namespace {
 #include "../priskv_amd/csrc/crc_device.inc"
+#include "crc_rows_explore.inc"
 #include "crc_dyn_explore.inc"
 #include "crc_pair_explore.inc"
 #include "crc_tail_explore.inc"
 #include "crc_rows2_explore.inc"
+#include "crc_steal_explore.inc"
 
 // read-only roof with the rows kernel's loop and addressing (same loads, no hashing)
 // TIMING: also write each wave's start / end s_memrealtime after the sink
-// words (as crc_rows_kernel's OPT bit 3)
+// words (as crc_rows_x_kernel's OPT bit 3)
 template <int G, int CH, int NBUF, int AUX, bool TIMING = false>
 __global__ __launch_bounds__(kThreads, rows_min_wg(CH, NBUF)) void roof_rows(const uint8_t *__restrict__ base, uint64_t ngroups,
                                                          uint32_t block_size, const uint32_t *, const uint32_t *,
@@ -98,6 +101,78 @@ __global__ __launch_bounds__(kThreads, rows_min_wg(CH, NBUF)) void roof_rows(con
     }
 }
 
+// read-only roof, block-cyclic: wave w reads tiles w, w + W, w + 2W, ...
+// of TILE groups each (contiguous inside a tile), so at any moment the chip
+// touches a window of about W * TILE groups instead of W ranges spread over
+// the whole buffer (TLB reach at 64-128 GiB)
+template <int G, int CH, int NBUF, int AUX, int TILE>
+__global__ __launch_bounds__(kThreads, rows_min_wg(CH, NBUF)) void roof_cyclic(const uint8_t *__restrict__ base,
+                                                                              uint64_t ngroups, uint32_t block_size,
+                                                                              const uint32_t *, const uint32_t *,
+                                                                              uint32_t *__restrict__ out, uint32_t)
+{
+    constexpr int NB = 64 / G, RB = 16 * G;
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint64_t W = (uint64_t)gridDim.x * kWaves;
+    const uint64_t wid = (uint64_t)blockIdx.x * kWaves + wave;
+    const uint64_t ntiles = ngroups / TILE; // host: ngroups % TILE == 0
+    const uint64_t mytiles = ntiles > wid ? (ntiles - wid + W - 1) / W : 0;
+    if (!mytiles)
+        return;
+    const uint32_t cps = block_size / (CH * RB);
+    const uint32_t nq = __builtin_amdgcn_readfirstlane((uint32_t)(mytiles * TILE * cps));
+    const uint32_t span = (NB - 1) * block_size + CH * RB;
+    const uint32_t voff = (uint32_t)(lane / G) * block_size + (uint32_t)(lane % G) * 16;
+    const uint64_t gstride = (uint64_t)NB * block_size;
+    const uint32_t cstride = CH * RB;
+    const uint8_t *pp = base + wid * TILE * gstride;
+    uint32_t pc = 0, pq = 0, pg = 0;
+    auto advance = [&]() {
+        if (pq + 1 < nq) {
+            pq++;
+            if (++pc == cps) {
+                pc = 0;
+                if (++pg == TILE) {
+                    pg = 0;
+                    pp += (W - 1) * TILE * gstride + gstride - (uint64_t)(cps - 1) * cstride;
+                } else {
+                    pp += gstride - (uint64_t)(cps - 1) * cstride;
+                }
+            } else {
+                pp += cstride;
+            }
+        }
+    };
+    v4u buf[NBUF][CH];
+#pragma unroll
+    for (int j = 0; j < NBUF - 1; j++) {
+        load_chunk<CH, RB, AUX>(buf[j], pp, span, voff);
+        advance();
+    }
+    uint32_t acc = 0, q = 0;
+    for (; q + NBUF <= nq; q += NBUF) {
+#pragma unroll
+        for (int j = 0; j < NBUF; j++) {
+            load_chunk<CH, RB, AUX>(buf[(j + NBUF - 1) % NBUF], pp, span, voff);
+            advance();
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int k = 0; k < CH; k++)
+                acc ^= buf[j][k].x ^ buf[j][k].y ^ buf[j][k].z ^ buf[j][k].w;
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < NBUF - 1; j++) {
+        if (q + j >= nq)
+            break;
+#pragma unroll
+        for (int k = 0; k < CH; k++)
+            acc ^= buf[j][k].x ^ buf[j][k].y ^ buf[j][k].z ^ buf[j][k].w;
+    }
+    out[wid * 64 + lane] = acc;
+}
+
 __global__ __launch_bounds__(256) void roof_gridstride(const v4u *__restrict__ p, uint64_t n16,
                                                        uint32_t *__restrict__ out)
 {
@@ -159,10 +234,19 @@ struct Variant {
             CH, WGPC, OPT,                                                                                     \
             [](dim3 g, hipStream_t s, const uint8_t *b, uint64_t n, uint32_t bs, const uint32_t *img,           \
                const uint32_t *fold, uint32_t *o) {                                                            \
-                hipLaunchKernelGGL((crc_rows_kernel<G, CH, NB, AUX, OPT>), g, dim3(kThreads), 0, s, b, n, bs, img, \
+                hipLaunchKernelGGL((crc_rows_x_kernel<G, CH, NB, AUX, OPT>), g, dim3(kThreads), 0, s, b, n, bs, img, \
                                    fold, o, (uint32_t)(((WE) << 16) | (WO)));                                  \
             }, {}}
 #define CRC_VARIANT(G, CH, NB, AUX, WGPC, OPT) CRC_VARIANT_W(G, CH, NB, AUX, WGPC, OPT, 0, 0)
+// the product kernel itself (priskv_amd/csrc/crc_device.inc crc_rows_kernel,
+// product OPT bits only) with the nibble image when OPT has bit 5
+#define PROD_VARIANT(G, CH, NB, OPT, WE, WO)                                                                  \
+    Variant{"prod G" #G " CH" #CH " NBUF" #NB " opt" #OPT " xw" #WE ":" #WO, true, G, CH, 1, OPT,              \
+            [](dim3 g, hipStream_t s, const uint8_t *b, uint64_t n, uint32_t bs, const uint32_t *img,           \
+               const uint32_t *fold, uint32_t *o) {                                                            \
+                hipLaunchKernelGGL((crc_rows_kernel<G, CH, NB, 2, OPT>), g, dim3(kThreads), 0, s, b, n, bs, img,   \
+                                   ((OPT) & 32) ? g_nib[G] : fold, o, (uint32_t)(((WE) << 16) | (WO)));        \
+            }, {}}
 // oversubscribed: K workgroups per CU in the grid, 32 KiB of dynamic LDS on
 // top of the 64 KiB tables so only ONE is resident per CU -- the hardware
 // dispatcher then hands each CU its next workgroup as it frees up (dynamic
@@ -172,7 +256,7 @@ struct Variant {
             CH, K, OPT,                                                                                        \
             [](dim3 g, hipStream_t s, const uint8_t *b, uint64_t n, uint32_t bs, const uint32_t *img,           \
                const uint32_t *fold, uint32_t *o) {                                                            \
-                hipLaunchKernelGGL((crc_rows_kernel<G, CH, NB, AUX, OPT>), g, dim3(kThreads), 32768, s, b, n, bs,  \
+                hipLaunchKernelGGL((crc_rows_x_kernel<G, CH, NB, AUX, OPT>), g, dim3(kThreads), 32768, s, b, n, bs,  \
                                    img, fold, o, (uint32_t)(((WE) << 16) | (WO)));                             \
             }, {}}
 #define ROOF_VARIANT_OS(G, CH, NB, AUX, K)                                                                    \
@@ -238,6 +322,13 @@ static uint32_t g_epoch = 0;
                                    (uint32_t)(((WE) << 16) | (WO)));                                       \
             }, {}}
 #define ROOF_VARIANT(G, CH, NB, AUX, WGPC) ROOF_VARIANT_W(G, CH, NB, AUX, WGPC, 0, 0)
+#define ROOFC_VARIANT(G, CH, NB, AUX, TILE)                                                                 \
+    Variant{"roofcyc G" #G " CH" #CH " NBUF" #NB " AUX" #AUX " tile" #TILE, false, G, CH, 1, -1,           \
+            [](dim3 g, hipStream_t s, const uint8_t *b, uint64_t n, uint32_t bs, const uint32_t *img,       \
+               const uint32_t *fold, uint32_t *o) {                                                        \
+                hipLaunchKernelGGL((roof_cyclic<G, CH, NB, AUX, TILE>), g, dim3(kThreads), 0, s, b, n, bs, img, fold, \
+                                   o, 0u);                                                                 \
+            }, {}}
 // roof with per-wave timing: writes into the CRC output buffer (is_crc for
 // the buffer choice, opt 8 for the timing report; excluded from the
 // bit-identity check by the is_crc/opt logic below)
@@ -251,6 +342,19 @@ static uint32_t g_epoch = 0;
             }, {}}
 // nibble-table fold (OPT bit 5): the fold pointer is the nibble image
 static uint32_t *g_nib[65] = {};
+// work stealing (crc_steal_explore.inc): claim words + a 4-bit launch epoch
+static uint64_t *g_claims = nullptr;
+static uint32_t g_epoch_s = 0;
+#define STEAL_VARIANT(G, CH, NB, AUX, OPT, WE, WO, T16, U)                                                     \
+    Variant{"steal G" #G " CH" #CH " NBUF" #NB " opt" #OPT " xw" #WE ":" #WO " t" #T16 " u" #U, true, G, CH, 1, \
+            (OPT),                                                                                             \
+            [](dim3 g, hipStream_t s, const uint8_t *b, uint64_t n, uint32_t bs, const uint32_t *img,           \
+               const uint32_t *fold, uint32_t *o) {                                                            \
+                g_epoch_s = (g_epoch_s + 1) & 15u;                                                             \
+                hipLaunchKernelGGL((crc_rows_steal_kernel<G, CH, NB, AUX, OPT>), g, dim3(kThreads), 0, s, b, n, bs, \
+                                   img, ((OPT) & 32) ? g_nib[G] : fold, o, (uint32_t)(((WE) << 16) | (WO)),     \
+                                   g_claims, (g_epoch_s << 28) | ((uint32_t)(T16) << 16) | (uint32_t)(U));      \
+            }, {}}
 // slice-by-8 pairs (OPT bit 6): 128 KiB image [Z_4 sets | Z_8 sets]
 static uint32_t *g_img8[65] = {};
 #define S8_VARIANT_W(G, CH, NB, AUX, WGPC, OPT, WE, WO)                                                       \
@@ -258,7 +362,7 @@ static uint32_t *g_img8[65] = {};
             CH, WGPC, OPT,                                                                                     \
             [](dim3 g, hipStream_t s, const uint8_t *b, uint64_t n, uint32_t bs, const uint32_t *,              \
                const uint32_t *, uint32_t *o) {                                                                \
-                hipLaunchKernelGGL((crc_rows_kernel<G, CH, NB, AUX, (OPT) | 32 | 64>), g, dim3(kThreads), 0, s, b, n, \
+                hipLaunchKernelGGL((crc_rows_x_kernel<G, CH, NB, AUX, (OPT) | 32 | 64>), g, dim3(kThreads), 0, s, b, n, \
                                    bs, g_img8[G], g_nib[G], o, (uint32_t)(((WE) << 16) | (WO)));               \
             }, {}}
 #define NIB_VARIANT_W(G, CH, NB, AUX, WGPC, OPT, WE, WO)                                                      \
@@ -266,7 +370,7 @@ static uint32_t *g_img8[65] = {};
             CH, WGPC, OPT,                                                                                     \
             [](dim3 g, hipStream_t s, const uint8_t *b, uint64_t n, uint32_t bs, const uint32_t *img,           \
                const uint32_t *, uint32_t *o) {                                                                \
-                hipLaunchKernelGGL((crc_rows_kernel<G, CH, NB, AUX, (OPT) | 32>), g, dim3(kThreads), 0, s, b, n, bs, \
+                hipLaunchKernelGGL((crc_rows_x_kernel<G, CH, NB, AUX, (OPT) | 32>), g, dim3(kThreads), 0, s, b, n, bs, \
                                    img, g_nib[G], o, (uint32_t)(((WE) << 16) | (WO)));                         \
             }, {}}
 
@@ -276,7 +380,7 @@ static uint32_t *g_img8[65] = {};
             (OPT) | 1024,                                                                                      \
             [](dim3 g, hipStream_t s, const uint8_t *b, uint64_t n, uint32_t bs, const uint32_t *img,           \
                const uint32_t *, uint32_t *o) {                                                                \
-                hipLaunchKernelGGL((crc_rows_kernel<G, CH, NB, AUX, (OPT) | 32 | 1024>), g, dim3(1024), 0, s, b, n, \
+                hipLaunchKernelGGL((crc_rows_x_kernel<G, CH, NB, AUX, (OPT) | 32 | 1024>), g, dim3(1024), 0, s, b, n, \
                                    bs, img, g_nib[G], o, (uint32_t)(((WE) << 16) | (WO)));                     \
             }, {}}
 #define CRC16_VARIANT_W(G, CH, NB, AUX, OPT, WE, WO)                                                          \
@@ -284,7 +388,7 @@ static uint32_t *g_img8[65] = {};
             (OPT) | 1024,                                                                                      \
             [](dim3 g, hipStream_t s, const uint8_t *b, uint64_t n, uint32_t bs, const uint32_t *img,           \
                const uint32_t *fold, uint32_t *o) {                                                            \
-                hipLaunchKernelGGL((crc_rows_kernel<G, CH, NB, AUX, (OPT) | 1024>), g, dim3(1024), 0, s, b, n, bs,  \
+                hipLaunchKernelGGL((crc_rows_x_kernel<G, CH, NB, AUX, (OPT) | 1024>), g, dim3(1024), 0, s, b, n, bs,  \
                                    img, fold, o, (uint32_t)(((WE) << 16) | (WO)));                             \
             }, {}}
 
@@ -418,10 +522,77 @@ int main(int argc, char **argv)
     CK(hipMalloc(&g_ctr, 4096));
     CK(hipMalloc(&g_slots, (size_t)ncu * 2 * kWaves * 128));
     CK(hipMemset(g_slots, 0, (size_t)ncu * 2 * kWaves * 128));
+    CK(hipMalloc(&g_claims, (size_t)ncu * 16 * 8));
+    CK(hipMemset(g_claims, 0, (size_t)ncu * 16 * 8));
     std::vector<Variant> all;
     // first entry = product reference for the bit-exact cross-check and the sustained run
     all.push_back(CRC_VARIANT_W(32, 8, 2, 2, 1, 2, 31, 29));
-    all.push_back(NIB_VARIANT_W(32, 8, 2, 2, 1, 2, 31, 29));
+    all.push_back(NIB_VARIANT_W(32, 8, 2, 2, 1, 2 | 768, 31, 29));
+    all.push_back(NIB_VARIANT_W(32, 8, 2, 2, 1, 2 | 768 | 8, 31, 29));
+    all.push_back(PROD_VARIANT(64, 4, 3, 2 | 32 | 768, 31, 29));
+    all.push_back(PROD_VARIANT(64, 4, 2, 32 | 256, 31, 29));
+    all.push_back(PROD_VARIANT(64, 4, 2, 256, 31, 29));
+    all.push_back(PROD_VARIANT(64, 4, 2, 768, 31, 29));
+    all.push_back(NIB_VARIANT_W(64, 4, 3, 2, 1, 2 | 768, 0, 0));
+    all.push_back(NIB_VARIANT_W(64, 4, 3, 2, 1, 2 | 768, 61, 59));
+    all.push_back(NIB_VARIANT_W(64, 4, 3, 2, 1, 2 | 768, 15, 13));
+    all.push_back(NIB_VARIANT_W(64, 4, 3, 2, 1, 2 | 512, 31, 29));
+    all.push_back(NIB_VARIANT_W(64, 4, 3, 2, 1, 2 | 256, 31, 29));
+    all.push_back(NIB_VARIANT_W(64, 4, 3, 2, 1, 2, 31, 29));
+    all.push_back(NIB_VARIANT_W(64, 4, 5, 2, 1, 2 | 768, 31, 29));
+    all.push_back(NIB_VARIANT_W(64, 4, 3, 2, 1, 2 | 768 | 8, 31, 29));
+    all.push_back(NIB_VARIANT_W(64, 4, 3, 2, 1, 2 | 769, 31, 29));
+    all.push_back(CRC_VARIANT_W(64, 4, 3, 2, 1, 768, 31, 29));
+    all.push_back(CRC_VARIANT_W(64, 4, 3, 2, 1, 0, 31, 29));
+    all.push_back(CRC_VARIANT_W(64, 4, 4, 2, 1, 768, 31, 29));
+    all.push_back(NIB_VARIANT_W(64, 4, 3, 2, 1, 256, 31, 29));
+    all.push_back(NIB_VARIANT_W(64, 4, 3, 2, 1, 768, 31, 29));
+    all.push_back(NIB_VARIANT_W(16, 4, 3, 2, 1, 2 | 768, 31, 29));
+    all.push_back(NIB_VARIANT_W(16, 4, 3, 2, 1, 2 | 256, 31, 29));
+    all.push_back(NIB_VARIANT_W(32, 4, 3, 2, 1, 256, 31, 29));
+    all.push_back(NIB_VARIANT_W(32, 4, 3, 2, 1, 0, 31, 29));
+    all.push_back(NIB_VARIANT_W(32, 4, 3, 2, 1, 769, 31, 29));
+    all.push_back(NIB_VARIANT_W(32, 4, 3, 2, 1, 768, 0, 0));
+    all.push_back(NIB_VARIANT_W(32, 4, 3, 2, 1, 768, 8, 7));
+    all.push_back(NIB_VARIANT_W(32, 4, 3, 2, 1, 768, 61, 59));
+    all.push_back(NIB_VARIANT_W(32, 2, 6, 2, 1, 768, 31, 29));
+    all.push_back(NIB_VARIANT_W(32, 2, 4, 2, 1, 768, 31, 29));
+    all.push_back(NIB_VARIANT_W(32, 2, 5, 2, 1, 768, 31, 29));
+    all.push_back(NIB_VARIANT_W(16, 8, 3, 2, 1, 768, 31, 29));
+    all.push_back(NIB_VARIANT_W(16, 4, 4, 2, 1, 768, 31, 29));
+    all.push_back(NIB_VARIANT_W(16, 4, 3, 2, 1, 768, 31, 29));
+    all.push_back(NIB_VARIANT_W(64, 4, 3, 2, 1, 2 | 768, 31, 29));
+    all.push_back(NIB_VARIANT_W(64, 4, 4, 2, 1, 2 | 768, 31, 29));
+    all.push_back(NIB_VARIANT_W(64, 2, 4, 2, 1, 768, 31, 29));
+    all.push_back(NIB_VARIANT_W(32, 4, 3, 2, 1, 768 | 8, 31, 29));
+    all.push_back(NIB_VARIANT_W(32, 8, 3, 2, 1, 2 | 768, 31, 29));
+    all.push_back(NIB_VARIANT_W(32, 8, 4, 2, 1, 2 | 768, 31, 29));
+    all.push_back(NIB_VARIANT_W(32, 4, 4, 2, 1, 768, 31, 29));
+    all.push_back(NIB_VARIANT_W(32, 4, 3, 2, 1, 768, 31, 29));
+    all.push_back(NIB_VARIANT_W(32, 4, 2, 2, 1, 768, 31, 29));
+    all.push_back(NIB_VARIANT_W(32, 8, 3, 2, 1, 2 | 256, 31, 29));
+    all.push_back(CRC_VARIANT_W(64, 4, 3, 2, 1, 256, 31, 29));
+    all.push_back(CRC_VARIANT_W(64, 4, 4, 2, 1, 256, 31, 29));
+    all.push_back(CRC_VARIANT_W(64, 8, 2, 2, 1, 256, 31, 29));
+    all.push_back(ROOFC_VARIANT(64, 4, 2, 2, 1));
+    all.push_back(ROOFC_VARIANT(64, 4, 2, 2, 4));
+    all.push_back(ROOFC_VARIANT(64, 4, 2, 2, 16));
+    all.push_back(ROOFC_VARIANT(32, 8, 2, 2, 8));
+    all.push_back(ROOFC_VARIANT(32, 8, 2, 2, 32));
+    all.push_back(ROOFC_VARIANT(32, 8, 2, 2, 128));
+    all.push_back(STEAL_VARIANT(32, 8, 2, 2, 2 | 32 | 768, 31, 29, 4, 8));
+    all.push_back(STEAL_VARIANT(32, 8, 2, 2, 2 | 32 | 768, 31, 29, 4, 16));
+    all.push_back(STEAL_VARIANT(32, 8, 2, 2, 2 | 32 | 768, 31, 29, 2, 8));
+    all.push_back(STEAL_VARIANT(32, 8, 2, 2, 2 | 32 | 768, 31, 29, 8, 8));
+    all.push_back(STEAL_VARIANT(32, 8, 2, 2, 2 | 32 | 768, 31, 29, 4, 4));
+    all.push_back(STEAL_VARIANT(32, 8, 2, 2, 2 | 32 | 768, 0, 0, 4, 8));
+    all.push_back(STEAL_VARIANT(32, 8, 2, 2, 2 | 32 | 768, 31, 29, 16, 8));
+    all.push_back(STEAL_VARIANT(32, 8, 2, 2, 2 | 32 | 768 | 8, 31, 29, 4, 8));
+    all.push_back(STEAL_VARIANT(64, 4, 2, 2, 256, 31, 29, 4, 1));
+    all.push_back(STEAL_VARIANT(64, 4, 2, 2, 256, 31, 29, 2, 1));
+    all.push_back(STEAL_VARIANT(64, 4, 2, 2, 256, 31, 29, 4, 2));
+    all.push_back(STEAL_VARIANT(64, 4, 2, 2, 256 | 8, 31, 29, 4, 1));
+    all.push_back(CRC_VARIANT_W(64, 4, 2, 2, 1, 256 | 8, 31, 29));
     all.push_back(S8_VARIANT_W(32, 8, 2, 2, 1, 2, 31, 29));
     all.push_back(NIB_VARIANT_W(32, 8, 2, 2, 1, 2, 0, 0));
     all.push_back(NIB_VARIANT_W(32, 8, 2, 2, 1, 2, 61, 59));

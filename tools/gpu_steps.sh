@@ -1,0 +1,76 @@
+#!/bin/bash
+# tools/gpu_steps.sh -- the one GPU-box runner (it replaces round 1's 105
+# one-off tools/gpu_r*.sh scripts; those stay in git history).
+#
+#   gpurun --timeout S -- 'bash tools/gpu_steps.sh TAG STEP [STEP ...]'
+#
+# Output goes to gpurun_out/TAG/.  Steps run in order, each under its own time
+# limit; the script stops at the first failing step (set -e), so nothing runs
+# on the GPU after a fault, an abort or a time limit.
+#
+#   tests                 pytest -m gpu over every GPU test (+ smoke, C executables)
+#   tests:EXPR            pytest -m gpu -k EXPR
+#   bench[:A,B,...]       python bench.py A B ...  (commas stand for spaces)
+#   explore:BS:NB:R:F     tools/crc_explore BS NB R with EXPLORE_FILTER=F
+#   ranges:ARGS           tools/ranges_explore ARGS (commas for spaces)
+#   paths:ARGS            python tools/bench_paths.py ARGS (commas for spaces)
+#   ktrace[:A,B,...]      rocprofv3 --kernel-trace --stats over bench.py A B ...
+#   pmc:C1+C2[:A,B,...]   one rocprofv3 --pmc pass (counters C1 C2 ...) over bench.py A B ...
+set -euo pipefail
+R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
+TAG=$1
+shift
+O=$R/gpurun_out/$TAG
+mkdir -p "$O"
+cd "$R"
+n=0
+for step in "$@"; do
+    n=$((n + 1))
+    kind=${step%%:*}
+    arg=""
+    [[ "$step" == *:* ]] && arg=${step#*:}
+    echo "[$n] $step" >&2
+    case "$kind" in
+    tests)
+        k=()
+        [[ -n "$arg" ]] && k=(-k "$arg")
+        timeout -k 10 900 python -u -m pytest tests -x -v -m gpu --timeout 300 --timeout-method thread "${k[@]}" \
+            > "$O/pytest_$n.log" 2>&1
+        if [[ -z "$arg" ]]; then
+            timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > "$O/smoke.log" 2>&1
+            timeout -k 10 120 ./tests/c/test_crc_gpu > "$O/c_gpu.log" 2>&1
+        fi
+        ;;
+    bench)
+        timeout -k 10 400 python -u bench.py ${arg//,/ } > "$O/bench_$n.json" 2> "$O/bench_$n.err"
+        ;;
+    explore)
+        IFS=: read -r bs nb rounds filt <<< "$arg"
+        EXPLORE_FILTER="$filt" timeout -k 10 300 ./tools/crc_explore "$bs" "$nb" "$rounds" > "$O/explore_$n.log" 2>&1
+        ;;
+    ranges)
+        timeout -k 10 300 ./tools/ranges_explore ${arg//,/ } > "$O/ranges_$n.log" 2>&1
+        ;;
+    paths)
+        timeout -k 10 400 python -u tools/bench_paths.py ${arg//,/ } > "$O/paths_$n.jsonl" 2> "$O/paths_$n.err"
+        ;;
+    ktrace)
+        (cd /tmp && export TMPDIR=/tmp &&
+            timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$O/ktrace_$n" -o run --output-format csv \
+                -- python3 "$R/bench.py" ${arg//,/ } > "$O/ktrace_$n.json" 2> "$O/ktrace_$n.err")
+        ;;
+    pmc)
+        ctrs=${arg%%:*}
+        bargs=""
+        [[ "$arg" == *:* ]] && bargs=${arg#*:}
+        (cd /tmp && export TMPDIR=/tmp &&
+            timeout -s KILL 180 rocprofv3 --pmc ${ctrs//+/ } -d "$O/pmc_$n" -o run --output-format csv \
+                -- python3 "$R/bench.py" ${bargs//,/ } > "$O/pmc_$n.json" 2> "$O/pmc_$n.err")
+        ;;
+    *)
+        echo "unknown step $step" >&2
+        exit 2
+        ;;
+    esac
+done
+echo ALLDONE >&2
