@@ -50,7 +50,8 @@ sys.path.insert(0, ROOT)
 METRIC = "GiB/s CRC over device-resident value blocks at 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
 SEED = 0x5EED5EED
-RAMP_S = 0.3
+RAMP_MIN_S = 1.0
+RAMP_MAX_S = 4.0
 COLD_IDLE_S = 1.0
 
 CONFIGS = {
@@ -104,18 +105,29 @@ def cpu_threads():
     return (min(avail, cap) if cap > 0 else avail), avail
 
 
-def ramp(fn, sync):
-    """The first ~10 launches after idle run up to 40 % slow while the device
-    leaves its idle power state (profiles/r01/clock_ramp.txt): keep stepping,
-    untimed, until RAMP_S seconds of back-to-back work have passed."""
+def ramp(fn, stream, torch, window=16, min_s=RAMP_MIN_S, max_s=RAMP_MAX_S):
+    """Untimed launches until the device is in its steady state.  A fresh
+    process runs 5-8 % slow for about its first second of GPU work, and the
+    first ~10 launches after idle up to 40 % (profiles/r01/clock_ramp.txt,
+    profiles/r02/bench_bisect_*.json): launch back-to-back windows of
+    `window` steps and stop once two consecutive windows agree within 0.5 %
+    (after at least min_s, at most max_s).  Returns (launches, seconds)."""
     n = 0
-    t_r = time.perf_counter()
-    while time.perf_counter() - t_r < RAMP_S:
-        for _ in range(4):
+    prev = None
+    t0 = time.perf_counter()
+    while True:
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for _ in range(window):
             fn(n)
             n += 1
-        sync()
-    return n
+        e1.record(stream)
+        e1.synchronize()
+        cur = e0.elapsed_time(e1)
+        el = time.perf_counter() - t0
+        if el >= max_s or (el >= min_s and prev is not None and abs(cur - prev) <= 0.005 * prev):
+            return n, el
+        prev = cur
 
 
 def main():
@@ -158,7 +170,10 @@ def main():
     region = torch.empty(bs * nb, dtype=torch.uint8, device=dev)
     ctx.fill_splitmix(region, SEED, word_offset=shard_word_offset(first, bs))
     out = torch.empty(nb, dtype=torch.int32, device=dev)
-    stream = torch.cuda.current_stream()
+    # a created stream: torch's null stream costs ~1 % per launch
+    # (profiles/r02/bench_bisect_*.json); the device-wide synchronize()
+    # around the timed region covers every stream
+    stream = torch.cuda.Stream(device=dev)
     sync = torch.cuda.synchronize
 
     def barrier():
@@ -168,23 +183,10 @@ def main():
     def step(_i=0):
         ctx.blocks_dev(region, bs, out=out, stream=stream)
 
-    # cold pass: the kernel's code object is loaded by a small call first,
-    # then the device idles COLD_IDLE_S and ONE full pass is timed -- what a
-    # one-off recovery scrub sees (clock ramp included)
-    ctx.blocks_dev(region, bs, out=out, stream=stream, nblocks=min(nb, 64))
-    sync()
-    time.sleep(COLD_IDLE_S)
-    ec0, ec1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    ec0.record(stream)
-    step()
-    ec1.record(stream)
-    sync()
-    cold_ms = ec0.elapsed_time(ec1)
-
     for _ in range(args.warmup):
         step()
     sync()
-    nramp = ramp(step, sync)
+    nramp, ramp_s = ramp(step, stream, torch)
 
     trace = os.environ.get("PRISKV_BENCH_TRACE")
     if trace:  # per-step kernel times of a separate, untimed pass (diagnostics only)
@@ -236,15 +238,12 @@ def main():
         "data": "synthetic (splitmix64 pattern filled on device)",
         "config": {"workload": desc, "block_size": bs, "nblocks_per_gpu": nb,
                    "bytes_per_gpu": bs * nb, "parallelism": f"shard{world} (contiguous block ranges, no collective)",
-                   "kernel": path, "untimed_ramp_launches": nramp,
+                   "kernel": path, "untimed_ramp_launches": nramp, "untimed_ramp_s": round(ramp_s, 2),
                    "also_measured": None if args.no_tib else CONFIGS["tib"][2] + " -> `tib`"},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": traffic, "kernel_ms": round(kernel_ms, 4),
                      "alg_bytes_per_launch": alg_bytes},
-        "cold_ms": round(cold_ms, 4),
-        "cold": {"ms": round(cold_ms, 4), "value": round(bs * nb / (cold_ms * 1e-3) / 2**30, 2), "unit": "GiB/s",
-                 "note": f"rank-local first pass after {COLD_IDLE_S:.1f} s idle (kernel already loaded)"},
     }
 
     if args.pipeline_streams > 1:
@@ -261,7 +260,8 @@ def main():
         def pstep(i):
             ctx.blocks_dev(region, bs, out=pouts[i % ns], stream=pstreams[i % ns])
 
-        ramp(pstep, sync)
+        ramp(pstep, stream, torch, window=2 * ns * 8, min_s=0.3)
+        sync()
         barrier()
         sync()
         tp0 = time.perf_counter()
@@ -290,6 +290,16 @@ def main():
     if not args.no_tib:
         result["tib"] = tib_leg(args, torch, ctx, dev, rank, world, barrier, O)
 
+    # cold pass, LAST on the GPU: the device idles COLD_IDLE_S and ONE full
+    # pass over a fresh region of the same shape is timed -- what a one-off
+    # recovery scrub sees (clock ramp included).  Measured last so that the
+    # idle cannot leave its slower first launches inside the other legs.
+    cold_ms = cold_pass(torch, ctx, dev, bs, nb, stream)
+    result["cold_ms"] = round(cold_ms, 4)
+    result["cold"] = {"ms": round(cold_ms, 4), "value": round(bs * nb / (cold_ms * 1e-3) / 2**30, 2), "unit": "GiB/s",
+                      "note": f"rank-local first pass after {COLD_IDLE_S:.1f} s idle (kernel already loaded), "
+                              f"measured after all other GPU work"}
+
     ok = bool(np.array_equal(O.crc32_blocks(host, bs, nthreads=8), gpu_crc))
     all_ok = max_over_ranks(0.0 if ok else 1.0, device=dev) == 0.0
     result["parity"] = {"checked_blocks_per_rank": nsamp, "bit_exact": bool(all_ok), "oracle": "oracle/crc_oracle.c"}
@@ -301,6 +311,25 @@ def main():
         print(json.dumps(result), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def cold_pass(torch, ctx, dev, bs, nb, stream):
+    """One full pass after the device has idled COLD_IDLE_S (fresh region of
+    the same shape, so nothing is cache-warm)."""
+    region = torch.empty(bs * nb, dtype=torch.uint8, device=dev)
+    ctx.fill_splitmix(region, SEED ^ 0xC01D)
+    out = torch.empty(nb, dtype=torch.int32, device=dev)
+    ctx.blocks_dev(region, bs, out=out, stream=stream, nblocks=min(nb, 64))
+    torch.cuda.synchronize()
+    time.sleep(COLD_IDLE_S)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    ctx.blocks_dev(region, bs, out=out, stream=stream)
+    e1.record(stream)
+    torch.cuda.synchronize()
+    del region, out
+    torch.cuda.empty_cache()
+    return e0.elapsed_time(e1)
 
 
 def tib_leg(args, torch, ctx, dev, rank, world, barrier, O):
@@ -316,14 +345,14 @@ def tib_leg(args, torch, ctx, dev, rank, world, barrier, O):
         return {"skipped": f"cannot allocate {bs * nb / 2**30:.0f} GiB: {e}"}
     ctx.fill_splitmix(region, SEED, word_offset=shard_word_offset(first, bs))
     out = torch.empty(nb, dtype=torch.int32, device=dev)
-    stream = torch.cuda.current_stream()
+    stream = torch.cuda.Stream(device=dev)
 
     def step(_i=0):
         ctx.blocks_dev(region, bs, out=out, stream=stream)
 
     step()
     torch.cuda.synchronize()
-    ramp(step, torch.cuda.synchronize)
+    ramp(step, stream, torch, window=3, min_s=0.5)
     k = max(1, args.tib_steps)
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     barrier()
@@ -347,11 +376,12 @@ def tib_leg(args, torch, ctx, dev, rank, world, barrier, O):
     ok = bool(np.array_equal(got, want))
     all_ok = max_over_ranks(0.0 if ok else 1.0, device=dev) == 0.0
     alg = nb * (bs + 4)
+    plan = ctx.blocks_plan(region.data_ptr(), nb, bs)
     del region, out
     torch.cuda.empty_cache()
     return {"workload": CONFIGS["tib"][2], "value": round(bs * nb * world * k / el / 2**30, 2), "unit": "GiB/s",
             "n_gpus": world, "steps": k, "ms_per_step": round(el / k * 1e3, 4), "bytes_per_gpu": bs * nb,
-            "kernel": ctx.blocks_plan(region.data_ptr(), nb, bs), "roofline": {"achieved": round(alg / (kms * 1e-3) / 1e9, 1),
+            "kernel": plan, "roofline": {"achieved": round(alg / (kms * 1e-3) / 1e9, 1),
                                                       "peak": HBM_PEAK_GBS, "unit": "GB/s",
                                                       "frac": round(alg / (kms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                                                       "kernel_ms": round(kms, 4)},

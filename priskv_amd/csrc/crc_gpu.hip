@@ -368,8 +368,9 @@ struct Plan {
 // 4 KiB: G64 / CH4 / NBUF3 replaced G32 / CH8 / NBUF2 in round 2 -- finer
 // chunks with three in flight keep more bytes in flight while a wave hashes;
 // +1.4-2.1 % in the explorer on two boxes, same process, bit-identical
-// (profiles/r02/explore_4k_*.log).  NBUF3 loses 1-3 % at 8 KiB-1 MiB
-// (profiles/r02/explore_{8k,64k,1m}_nbuf*.log), so those keep NBUF2.
+// (profiles/r02/explore_r2e_explore_4k_sweep_{a,b}.log, explore_r2f_4k_{a,b}.log).
+// NBUF3 loses 1-3 % at 8 KiB-1 MiB (profiles/r02/explore_r2f_{8k,64k,1m}.log),
+// so those keep NBUF2.
 constexpr int kPrio1 = 1 << 8, kPrio3 = 3 << 8;
 constexpr Plan kPlans[NPLANS] = {
     {64, 4, 3, 2 | 32 | kPrio3, 1, 31, 29}, {64, 4, 2, 32 | kPrio1, 1, 31, 29}, {16, 4, 2, 2 | 32 | kPrio1, 1, 31, 29},

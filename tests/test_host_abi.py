@@ -264,3 +264,69 @@ def test_host_out_arrays_are_checked():
     for bad in (np.empty(4, np.uint32), np.empty(8, np.int64), np.empty(16, np.uint32)[::2], [0] * 8):
         with pytest.raises(ValueError):
             _host_out(bad, 8)
+
+
+REF = "/root/reference"
+
+
+def _defined_globals(obj):
+    out = subprocess.run(["nm", "--defined-only", "-g", obj], capture_output=True, text=True, check=True).stdout
+    return {ln.split()[-1]: ln.split()[-2] for ln in out.splitlines() if len(ln.split()) == 3}
+
+
+@pytest.mark.skipif(not os.path.exists(os.path.join(REF, "server", "crc.c")), reason="reference not mounted")
+def test_reference_callers_link_against_dropin(tmp_path):
+    """libpriskv_crc_host.a as the drop-in for server/crc.o in the reference's
+    server link (server/Makefile:32-35,63-64), checked without building any
+    reference file that needs a header the image lacks.
+
+    server/kv.c itself cannot be compiled here: its include chain
+    (kv.h -> backend/backend.h -> list.h -> include/priskv-utils.h:45) needs
+    <uuid/uuid.h>, which this image does not have, and a stand-in header is
+    not allowed for a reference build.  What is checked instead:
+      1. crc.o -- the reference's own server/crc.c, compiled unmodified --
+         defines exactly one global, priskv_crc32, and the archive defines it
+         too, as a text (T) symbol: replacing crc.o leaves no undefined symbol;
+      2. a caller compiled against the reference's UNMODIFIED server/crc.h,
+         calling as server/kv.c:314,408 and server/rdma.c:764 do, links
+         against the archive and resolves priskv_crc32 to its member;
+      3. no other global the archive defines is defined anywhere in the
+         reference's server/, lib/ or client/ sources (no duplicate symbols);
+      4. the three reference call sites call priskv_crc32 by that name."""
+    archive = os.path.join(LIBDIR, "libpriskv_crc_host.a")
+    # 1. the reference's crc.o, built from the source where it lies (no copy)
+    crc_o = tmp_path / "crc.o"
+    subprocess.run(["gcc", "-O2", "-c", f"-I{REF}/server", f"{REF}/server/crc.c", "-o", str(crc_o)], check=True)
+    ref_syms = _defined_globals(str(crc_o))
+    assert ref_syms == {"priskv_crc32": "T"}, ref_syms
+    ours = _defined_globals(archive)
+    assert ours.get("priskv_crc32") == "T"
+    # 2. a caller against the reference's own header, kv.c's call shape
+    src = tmp_path / "kv_like_caller.c"
+    src.write_text(
+        '#include <stdio.h>\n#include <stdint.h>\n#include "crc.h"\n'  # resolves to /root/reference/server/crc.h
+        "static unsigned bucket(uint8_t *key, uint16_t keylen, unsigned count) {\n"
+        "  return priskv_crc32(key, keylen) % count; /* server/kv.c:314,408 */\n}\n"
+        "int main(void) {\n  uint8_t k[] = \"123456789\";\n"
+        "  printf(\"%u\\n\", bucket(k, 9, 1000003u));\n"
+        "  return priskv_crc32(k, 9) == 0x2dfd2d88u ? 0 : 1;\n}\n")
+    exe = tmp_path / "caller"
+    r = subprocess.run(["gcc", "-O2", "-Wall", "-Werror", f"-I{REF}/server", str(src), archive, "-lpthread",
+                        "-Wl,--trace-symbol=priskv_crc32", "-o", str(exe)], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    assert "libpriskv_crc_host.a(crc_host.o): definition of priskv_crc32" in r.stdout + r.stderr, r.stdout + r.stderr
+    assert subprocess.run([str(exe)]).returncode == 0
+    # 3. no other archive global is defined by the reference's sources
+    others = set(ours) - {"priskv_crc32"}
+    clashes = []
+    for top in ("server", "lib", "client"):
+        for dirpath, _, files in os.walk(os.path.join(REF, top)):
+            for f in files:
+                if f.endswith((".c", ".h")):
+                    text = open(os.path.join(dirpath, f), errors="replace").read()
+                    clashes += [(f, s) for s in others if re.search(rf"\b{re.escape(s)}\s*\(", text)]
+    assert not clashes, clashes
+    # 4. the reference's call sites (SURVEY §3)
+    for path, line in (("server/kv.c", 314), ("server/kv.c", 408), ("server/rdma.c", 764)):
+        with open(os.path.join(REF, path)) as fh:
+            assert "priskv_crc32(" in fh.readlines()[line - 1], (path, line)

@@ -14,6 +14,8 @@
 #   explore:BS:NB:R:F     tools/crc_explore BS NB R with EXPLORE_FILTER=F
 #   ranges:ARGS           tools/ranges_explore ARGS (commas for spaces)
 #   paths:ARGS            python tools/bench_paths.py ARGS (commas for spaces)
+#   lib:ARGS              tools/lib_timing ARGS: blocks_dev through the C ABI, no torch
+#   py:SCRIPT[:ARGS]      python tools/SCRIPT ARGS (commas for spaces)
 #   ktrace[:A,B,...]      rocprofv3 --kernel-trace --stats over bench.py A B ...
 #   pmc:C1+C2[:A,B,...]   one rocprofv3 --pmc pass (counters C1 C2 ...) over bench.py A B ...
 set -euo pipefail
@@ -53,6 +55,15 @@ for step in "$@"; do
         ;;
     paths)
         timeout -k 10 400 python -u tools/bench_paths.py ${arg//,/ } > "$O/paths_$n.jsonl" 2> "$O/paths_$n.err"
+        ;;
+    lib)
+        timeout -k 10 200 ./tools/lib_timing ${arg//,/ } > "$O/lib_$n.json" 2> "$O/lib_$n.err"
+        ;;
+    py)
+        script=${arg%%:*}
+        pargs=""
+        [[ "$arg" == *:* ]] && pargs=${arg#*:}
+        timeout -k 10 400 python -u "tools/$script" ${pargs//,/ } > "$O/py_$n.out" 2> "$O/py_$n.err"
         ;;
     ktrace)
         (cd /tmp && export TMPDIR=/tmp &&
