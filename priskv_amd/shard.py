@@ -29,9 +29,11 @@ def shard_blocks(nblocks: int, rank: int, world: int) -> Tuple[int, int]:
 def shard_word_offset(first_block: int, block_size: int) -> int:
     """Splitmix64 word index where a shard starting at ``first_block`` begins
     (test pattern of priskv_crc_fill_splitmix_dev), so the shards of all ranks
-    are slices of one global region.  Needs block_size % 8 == 0."""
-    if block_size % 8:
-        raise ValueError("pattern word offsets need 8-byte aligned block starts")
+    are slices of one global region.  Needs the shard to start on an 8-byte
+    boundary of that region (always true for rank 0, and for every rank when
+    block_size % 8 == 0)."""
+    if (first_block * block_size) % 8:
+        raise ValueError("pattern word offsets need 8-byte aligned shard starts")
     return first_block * block_size // 8
 
 
