@@ -73,6 +73,8 @@ struct priskv_crc_ctx {
     int balance;               // byte-balanced extents split (PRISKV_CRC_BALANCE=0: off)
     uint64_t seg_max_extents;  // device-resident lengths: segment calls of at most this many extents
     int xcd_rr;                // the XCD probe found workgroup b on XCD b % 8 (weights apply)
+    uint64_t tile_min_bytes;   // rows batches of at least this many bytes run in block-cyclic tiles
+    uint64_t tile_bytes;       // ... of about this many bytes each
     uint32_t *d_lds_image[3];  // 64 KiB each: set B gap for G = 64, 32, 16
     uint32_t *d_fold;          // kFoldSets x 2048 words, set j for G = 1 << j
     uint32_t *d_nibrep[7];     // nibble fold tables for G = 1 << j (j >= 1), 8 x 16 x max(G, 32) words
@@ -421,6 +423,26 @@ const void *plan_fn(int p, bool prio)
     }
 }
 
+// Block-cyclic tiles for big batches (crc_rows_kernel `tile`): groups per
+// tile, 0 = the contiguous per-wave split.  64 KiB blocks, 1 MiB tiles
+// against contiguous ranges, same box (profiles/r02/tiles/lib_*.json,
+// tools/lib_timing): 16 GiB 2.558 / 2.436 ms, 32 GiB 4.888 / 4.874,
+// 64 GiB 9.859 / 9.802, 128 GiB 20.04 / 21.38 (+6.7 % for tiles; +5.7 % in
+// the explorer on another box, explore_r2r_*).  On some boxes the contiguous
+// split already slows down at 64 GiB (explore_r2c_explore_64k_size_*), so
+// tiles start there.  PRISKV_CRC_TILE_MIN_GIB / PRISKV_CRC_TILE_KIB move the
+// switch and the tile size.
+constexpr uint64_t kTileMinBytes = 64ull << 30;
+constexpr uint64_t kTileBytes = 1ull << 20;
+
+uint32_t tile_groups(const priskv_crc_ctx *ctx, uint64_t ngroups, uint64_t gstride)
+{
+    if (ngroups * gstride < ctx->tile_min_bytes)
+        return 0;
+    const uint64_t t = ctx->tile_bytes / gstride;
+    return t ? (uint32_t)(t < (1u << 20) ? t : (1u << 20)) : 1u;
+}
+
 int launch_plan(const priskv_crc_ctx *ctx, int p, const uint8_t *base, uint64_t ngroups, uint32_t bs, uint32_t *out,
                 hipStream_t s)
 {
@@ -441,7 +463,9 @@ int launch_plan(const priskv_crc_ctx *ctx, int p, const uint8_t *base, uint64_t 
         const uint32_t *fold = (P.opt & 32) ? ctx->d_nibrep[log2u(P.G)] : ctx->d_fold + log2u(P.G) * 2048;
         // weights move whole groups: only worth it with many groups per wave
         uint32_t xw = n >= 32ull * grid * kWaves ? ctx->plan_xw[p] : 0u;
-        void *args[] = {(void *)&b, (void *)&n, (void *)&bs, (void *)&img, (void *)&fold, (void *)&o, (void *)&xw};
+        uint32_t tile = tile_groups(ctx, n, nb_per_group * bs);
+        void *args[] = {(void *)&b,    (void *)&n, (void *)&bs, (void *)&img, (void *)&fold,
+                        (void *)&o,    (void *)&xw, (void *)&tile};
         if (int rc = herr(hipLaunchKernel(plan_fn(p, ctx->prio), dim3(grid), dim3(kThreads), args, 0, s)))
             return rc;
         done += n;
@@ -752,7 +776,11 @@ int priskv_crc32_blocks_plan(const priskv_crc_ctx *ctx, const void *d_base, uint
                      (P.opt & 2) ? ",pipelined-fold" : "", (P.opt & 32) ? ",nibble-fold" : "");
         if (w >= 0 && (uint64_t)w < len && mode)
             w += snprintf(buf + w, len - w, ",progress-priority %d", mode);
-        if (w >= 0 && (uint64_t)w < len && xw)
+        const uint64_t ngroups = nblocks * S / (64 / P.G);
+        const uint32_t tile = tile_groups(ctx, ngroups, (uint64_t)(64 / P.G) * bs);
+        if (w >= 0 && (uint64_t)w < len && tile)
+            w += snprintf(buf + w, len - w, ",block-cyclic tiles of %u groups", tile);
+        else if (w >= 0 && (uint64_t)w < len && xw && ngroups >= 32ull * ctx->num_cus * ctx->plan_wgs_per_cu[p] * kWaves)
             w += snprintf(buf + w, len - w, ",xcd-weighted %u:%u", xw >> 16, xw & 0xFFFF);
         if (w >= 0 && (uint64_t)w < len)
             w += snprintf(buf + w, len - w, ">%s", S > 1 ? " x segments + crc_combine_segments_kernel" : "");
@@ -804,6 +832,14 @@ int priskv_crc_ctx_create(int device, priskv_crc_ctx **out)
         const char *be = getenv("PRISKV_CRC_BALANCE");
         c->balance = !(be && !strcmp(be, "0"));
         c->seg_max_extents = kSegMaxExtents;
+        c->tile_min_bytes = kTileMinBytes;
+        c->tile_bytes = kTileBytes;
+        if (const char *m = getenv("PRISKV_CRC_TILE_MIN_GIB"))
+            c->tile_min_bytes = strtoull(m, nullptr, 10) << 30;
+        if (const char *m = getenv("PRISKV_CRC_TILE_KIB")) {
+            const unsigned long long v = strtoull(m, nullptr, 10);
+            c->tile_bytes = v ? v << 10 : kTileBytes;
+        }
         if (const char *m = getenv("PRISKV_CRC_SEG_MAX_EXTENTS")) { // capped by the plan kernel's 16384
             const unsigned long long v = strtoull(m, nullptr, 10);
             const uint64_t cap = (uint64_t)kSegPlanThreads * kSegPlanPerThread;

@@ -951,18 +951,24 @@ def _ctx_env(**env):
                 os.environ[k] = v
 
 
-@pytest.mark.parametrize("bs", [4096, 8192, 65536, 1 << 20])
-def test_xcd_weights_and_probe_fallback(torch_cuda, ctx, bs):
+@pytest.mark.parametrize("bs", [1024, 4096, 8192, 65536])
+def test_xcd_weights_probe_fallback_and_tiles(torch_cuda, ctx, bs):
     """The XCD-weighted split (workgroup b assumed on XCD b % 8, checked by a
-    probe at context creation), an override, equal shares, and the probe's
-    forced fallback give the oracle's CRCs; the plan string says which split
-    each context uses."""
+    probe at context creation), an override, equal shares, the probe's forced
+    fallback, and block-cyclic tiles (forced on, small tiles so the last one
+    is short) give the oracle's CRCs; the plan string says which split each
+    context uses.  The batches hold >= 32 groups per resident wave, the size
+    from which the library applies the weights."""
     torch = torch_cuda
-    nb = max(64, (96 << 20) // bs) + 1
+    per = 64 // {1024: 16, 4096: 64, 8192: 64, 65536: 64}[bs]  # blocks per group of the plan
+    nb = 32 * 2048 * per + 5 * per + (per if bs == 65536 else 0)
+    if bs == 65536:
+        nb = 16 * 2048 + 3  # 2 GiB: weights need 4 GiB here, tiles are the point
     t = _region(torch, ctx, bs * nb, SEED ^ bs ^ 0x3C, nb)
-    want = O.crc32_blocks(t[: bs * nb].cpu().numpy(), bs, nthreads=8)
+    want = O.crc32_blocks(t[: bs * nb].cpu().numpy(), bs, nthreads=16)
     ctxs = {"default": ctx, "1:1": _ctx_env(PRISKV_CRC_XCD_WEIGHTS="1:1"),
-            "17:13": _ctx_env(PRISKV_CRC_XCD_WEIGHTS="17:13"), "fallback": _ctx_env(PRISKV_CRC_XCD_PROBE="0")}
+            "17:13": _ctx_env(PRISKV_CRC_XCD_WEIGHTS="17:13"), "fallback": _ctx_env(PRISKV_CRC_XCD_PROBE="0"),
+            "tiles": _ctx_env(PRISKV_CRC_TILE_MIN_GIB="0", PRISKV_CRC_TILE_KIB=str(max(64, 4 * bs >> 10)))}
     plans = {}
     for name, c in ctxs.items():
         got = _u32(c.blocks_dev(t, bs, nblocks=nb))
@@ -970,10 +976,12 @@ def test_xcd_weights_and_probe_fallback(torch_cuda, ctx, bs):
         assert np.array_equal(got, want), (name, np.nonzero(got != want)[0][:8])
         plans[name] = c.blocks_plan(t.data_ptr(), nb, bs)
     assert "xcd-weighted" not in plans["1:1"] and "xcd-weighted" not in plans["fallback"], plans
-    assert "xcd-weighted 17:13" in plans["17:13"], plans
-    # MI355X dispatches workgroups round-robin over its 8 XCDs: the probe agrees
-    assert "xcd-weighted 31:29" in plans["default"], plans
-    for name in ("1:1", "17:13", "fallback"):
+    assert "block-cyclic" in plans["tiles"] and "xcd-weighted" not in plans["tiles"], plans
+    if bs != 65536:
+        assert "xcd-weighted 17:13" in plans["17:13"], plans
+        # MI355X dispatches workgroups round-robin over its 8 XCDs: the probe agrees
+        assert "xcd-weighted 31:29" in plans["default"], plans
+    for name in ("1:1", "17:13", "fallback", "tiles"):
         ctxs[name].close()
 
 
@@ -983,6 +991,8 @@ def test_blocks_plan_strings(torch_cuda, ctx):
     assert ctx.blocks_plan(base, 1 << 20, 4096).startswith("crc_rows_kernel<G=64,CH=4,NBUF=3,nt,pipelined-fold,"
                                                              "nibble-fold,progress-priority 3")
     assert ctx.blocks_plan(base, 1 << 16, 65536).startswith("crc_rows_kernel<G=64,CH=4,NBUF=2,nt,progress-priority 1")
+    # the 128 GiB shard of BASELINE configs[3] runs in block-cyclic 1 MiB tiles
+    assert "block-cyclic tiles of 16 groups" in ctx.blocks_plan(base, 1 << 21, 65536)
     assert "segments" in ctx.blocks_plan(base, 1, 1 << 20)
     assert ctx.blocks_plan(base, 100, 256) == "crc_small_kernel<G=16>"
     assert ctx.blocks_plan(base + 1, 100, 4096) == "crc_ranges_kernel (extents)"

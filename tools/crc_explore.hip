@@ -245,7 +245,7 @@ struct Variant {
             [](dim3 g, hipStream_t s, const uint8_t *b, uint64_t n, uint32_t bs, const uint32_t *img,           \
                const uint32_t *fold, uint32_t *o) {                                                            \
                 hipLaunchKernelGGL((crc_rows_kernel<G, CH, NB, 2, OPT>), g, dim3(kThreads), 0, s, b, n, bs, img,   \
-                                   ((OPT) & 32) ? g_nib[G] : fold, o, (uint32_t)(((WE) << 16) | (WO)));        \
+                                   ((OPT) & 32) ? g_nib[G] : fold, o, (uint32_t)(((WE) << 16) | (WO)), 0u);    \
             }, {}}
 // oversubscribed: K workgroups per CU in the grid, 32 KiB of dynamic LDS on
 // top of the 64 KiB tables so only ONE is resident per CU -- the hardware
@@ -530,6 +530,14 @@ int main(int argc, char **argv)
     all.push_back(NIB_VARIANT_W(32, 8, 2, 2, 1, 2 | 768, 31, 29));
     all.push_back(NIB_VARIANT_W(32, 8, 2, 2, 1, 2 | 768 | 8, 31, 29));
     all.push_back(PROD_VARIANT(64, 4, 3, 2 | 32 | 768, 31, 29));
+    all.push_back(CRC_VARIANT_W(64, 4, 2, 2, 1, 256 | 8192, 0, 0));
+    all.push_back(CRC_VARIANT_W(64, 4, 2, 2, 1, 256 | 8192 | 16384, 0, 0));
+    all.push_back(CRC_VARIANT_W(64, 4, 2, 2, 1, 256 | 8192 | 32768, 0, 0));
+    all.push_back(CRC_VARIANT_W(64, 4, 2, 2, 1, 8192 | 16384, 0, 0));
+    all.push_back(NIB_VARIANT_W(64, 4, 3, 2, 1, 2 | 768 | 4096, 31, 29));
+    all.push_back(NIB_VARIANT_W(64, 4, 2, 2, 1, 256 | 4096, 31, 29));
+    all.push_back(CRC_VARIANT_W(64, 4, 2, 2, 1, 256 | 4096, 31, 29));
+    all.push_back(CRC_VARIANT_W(64, 4, 2, 2, 1, 768 | 4096, 31, 29));
     all.push_back(PROD_VARIANT(64, 4, 2, 32 | 256, 31, 29));
     all.push_back(PROD_VARIANT(64, 4, 2, 256, 31, 29));
     all.push_back(PROD_VARIANT(64, 4, 2, 768, 31, 29));

@@ -9,14 +9,17 @@
 # on the GPU after a fault, an abort or a time limit.
 #
 #   tests                 pytest -m gpu over every GPU test (+ smoke, C executables)
-#   tests:EXPR            pytest -m gpu -k EXPR
+#   tests:A,B             pytest -m gpu -k "A or B"
 #   bench[:A,B,...]       python bench.py A B ...  (commas stand for spaces)
 #   explore:BS:NB:R:F     tools/crc_explore BS NB R with EXPLORE_FILTER=F
 #   ranges:ARGS           tools/ranges_explore ARGS (commas for spaces)
 #   paths:ARGS            python tools/bench_paths.py ARGS (commas for spaces)
 #   lib:ARGS              tools/lib_timing ARGS: blocks_dev through the C ABI, no torch
+#   libenv:VAR=V:ARGS     the same with one environment variable set
 #   py:SCRIPT[:ARGS]      python tools/SCRIPT ARGS (commas for spaces)
+#   gloo2[:A,B,...]       2-rank rehearsal of bench.py's N>1 path on this one GPU (gloo)
 #   ktrace[:A,B,...]      rocprofv3 --kernel-trace --stats over bench.py A B ...
+#   ktracepy:SCRIPT[:A,B] rocprofv3 --kernel-trace --stats over python tools/SCRIPT A B ...
 #   pmc:C1+C2[:A,B,...]   one rocprofv3 --pmc pass (counters C1 C2 ...) over bench.py A B ...
 set -euo pipefail
 R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
@@ -35,7 +38,7 @@ for step in "$@"; do
     case "$kind" in
     tests)
         k=()
-        [[ -n "$arg" ]] && k=(-k "$arg")
+        [[ -n "$arg" ]] && k=(-k "${arg//,/ or }")
         timeout -k 10 900 python -u -m pytest tests -x -v -m gpu --timeout 300 --timeout-method thread "${k[@]}" \
             > "$O/pytest_$n.log" 2>&1
         if [[ -z "$arg" ]]; then
@@ -59,6 +62,12 @@ for step in "$@"; do
     lib)
         timeout -k 10 200 ./tools/lib_timing ${arg//,/ } > "$O/lib_$n.json" 2> "$O/lib_$n.err"
         ;;
+    libenv)
+        kv=${arg%%:*}
+        largs=""
+        [[ "$arg" == *:* ]] && largs=${arg#*:}
+        env "$kv" timeout -k 10 200 ./tools/lib_timing ${largs//,/ } > "$O/lib_$n.json" 2> "$O/lib_$n.err"
+        ;;
     py)
         script=${arg%%:*}
         pargs=""
@@ -69,6 +78,19 @@ for step in "$@"; do
         (cd /tmp && export TMPDIR=/tmp &&
             timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$O/ktrace_$n" -o run --output-format csv \
                 -- python3 "$R/bench.py" ${arg//,/ } > "$O/ktrace_$n.json" 2> "$O/ktrace_$n.err")
+        ;;
+    gloo2)
+        PRISKV_BENCH_BACKEND=gloo timeout -k 10 400 python -m torch.distributed.run --nnodes 1 --nproc-per-node 2 \
+            --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 2 ${arg//,/ } > "$O/gloo2_$n.json" \
+            2> "$O/gloo2_$n.err"
+        ;;
+    ktracepy)
+        script=${arg%%:*}
+        pargs=""
+        [[ "$arg" == *:* ]] && pargs=${arg#*:}
+        (cd /tmp && export TMPDIR=/tmp &&
+            timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$O/ktracepy_$n" -o run --output-format csv \
+                -- python3 "$R/tools/$script" ${pargs//,/ } > "$O/ktracepy_$n.out" 2> "$O/ktracepy_$n.err")
         ;;
     pmc)
         ctrs=${arg%%:*}
