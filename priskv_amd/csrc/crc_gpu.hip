@@ -99,6 +99,10 @@ struct priskv_crc_ctx {
     mutable pthread_mutex_t pool_lock;
     int pool_ready;
     mutable priskv_crc_pool_slot pool[NPOOL];
+    // the fused few-extents kernel's counters + partials (zeroed when
+    // allocated; the kernel leaves the counters zero; guarded by pool_lock)
+    mutable priskv_crc_pool_slot cnt_pool[NPOOL];
+    int fused;                 // few extents in one launch (PRISKV_CRC_FUSED=0: the three-launch path)
 };
 
 namespace {
@@ -139,12 +143,29 @@ inline int herr(hipError_t e)
 // per call against ~1 us for the event pair (profiles/r01/host_cost_r4k.json).
 // While the stream is capturing, or with every slot taken, it is a per-call
 // hipMallocAsync / hipFreeAsync as before, so a captured graph owns its own.
+//
+// zero: the memory must read as zeros when a call gets it.  Then `slots` is a
+// pool whose users leave their slot zeroed (the fused extents kernel's
+// counters): a new allocation is cleared once, a reused slot is not.
 struct Scratch {
     const priskv_crc_ctx *ctx;
     hipStream_t s;
+    priskv_crc_pool_slot *slots;
+    bool zero;
     int slot = -1;
     void *p = nullptr;
-    Scratch(const priskv_crc_ctx *c, hipStream_t st) : ctx(c), s(st) {}
+    Scratch(const priskv_crc_ctx *c, hipStream_t st) : ctx(c), s(st), slots(c->pool), zero(false) {}
+    Scratch(const priskv_crc_ctx *c, hipStream_t st, priskv_crc_pool_slot *pool_slots, bool zeroed)
+        : ctx(c), s(st), slots(pool_slots), zero(zeroed)
+    {
+    }
+    int zero_fill(void *q, size_t bytes)
+    {
+        const uint64_t nw = bytes / 4;
+        const uint32_t grid = (uint32_t)(nw / 256 + 1 < 1024 ? nw / 256 + 1 : 1024);
+        hipLaunchKernelGGL(crc_zero_kernel, dim3(grid), dim3(256), 0, s, static_cast<uint32_t *>(q), nw);
+        return herr(hipGetLastError());
+    }
     int get(size_t bytes)
     {
         hipStreamCaptureStatus cs = hipStreamCaptureStatusActive;
@@ -152,22 +173,22 @@ struct Scratch {
             pthread_mutex_lock(&ctx->pool_lock);
             int fit = -1, grow = -1; // smallest free slot that fits, else the largest free one
             for (int i = 0; i < NPOOL; i++) {
-                const priskv_crc_pool_slot &q = ctx->pool[i];
+                const priskv_crc_pool_slot &q = slots[i];
                 if (q.busy)
                     continue;
                 if (q.size >= bytes) {
-                    if (fit < 0 || q.size < ctx->pool[fit].size)
+                    if (fit < 0 || q.size < slots[fit].size)
                         fit = i;
-                } else if (grow < 0 || q.size > ctx->pool[grow].size) {
+                } else if (grow < 0 || q.size > slots[grow].size) {
                     grow = i;
                 }
             }
             const int k = fit >= 0 ? fit : grow;
             if (k >= 0)
-                ctx->pool[k].busy = 1;
+                slots[k].busy = 1;
             pthread_mutex_unlock(&ctx->pool_lock);
             if (k >= 0) {
-                priskv_crc_pool_slot &q = ctx->pool[k];
+                priskv_crc_pool_slot &q = slots[k];
                 int rc = q.used ? herr(hipStreamWaitEvent(s, q.ev, 0)) : 0;
                 if (!rc && q.size < bytes) {
                     size_t cap = 64u << 10;
@@ -179,6 +200,8 @@ struct Scratch {
                     q.size = 0;
                     if (!rc && !(rc = herr(hipMallocAsync(&q.p, cap, s))))
                         q.size = cap;
+                    if (!rc && zero)
+                        rc = zero_fill(q.p, cap);
                 }
                 if (rc) {
                     pthread_mutex_lock(&ctx->pool_lock);
@@ -191,14 +214,17 @@ struct Scratch {
                 return 0;
             }
         }
-        return herr(hipMallocAsync(&p, bytes, s));
+        int rc = herr(hipMallocAsync(&p, bytes, s));
+        if (!rc && zero)
+            rc = zero_fill(p, bytes);
+        return rc;
     }
     // after the call's work is enqueued on s
     int release()
     {
         if (slot < 0)
             return p ? herr(hipFreeAsync(p, s)) : 0;
-        priskv_crc_pool_slot &q = ctx->pool[slot];
+        priskv_crc_pool_slot &q = slots[slot];
         int rc = herr(hipEventRecord(q.ev, s));
         if (rc)
             (void)hipStreamSynchronize(s); // the slot is idle before anyone reuses it
@@ -299,6 +325,7 @@ int launch_ext_kernel(const priskv_crc_ctx *ctx, bool seg, bool many, bool bal, 
 }
 
 constexpr int kZpowRows = 48;
+static_assert(kZpowRows == kFusedZRows, "the fused kernel keeps every Z_(2^k) row in LDS");
 
 int launch_extents_seg(const priskv_crc_ctx *ctx, const uint8_t *base, uint64_t n, const uint64_t *offs,
                        const uint32_t *lens, uint64_t stride, uint32_t len_const, uint32_t *out, hipStream_t s,
@@ -529,6 +556,9 @@ int launch_rows_plain(const priskv_crc_ctx *ctx, const uint8_t *base, uint64_t n
 constexpr uint64_t kSegMaxExtents = 8192;
 constexpr uint64_t kSegPerWave = 8; // full segments per resident wave (tools/bench_paths.py few / ranges)
 constexpr uint32_t kSegMinLen = 64u << 10;
+// progress priority off in the fused kernel: 1 x 256 MiB 49.7 us vs 50.7 with
+// mode 3, 4096 small values 7.6 vs 7.7 us (profiles/r02/fused/ktrace_shapes_*)
+constexpr int kFusedPrio = 0;
 
 int launch_extents_seg(const priskv_crc_ctx *ctx, const uint8_t *base, uint64_t n, const uint64_t *offs,
                        const uint32_t *lens, uint64_t stride, uint32_t len_const, uint32_t *out, hipStream_t s,
@@ -547,6 +577,30 @@ int launch_extents_seg(const priskv_crc_ctx *ctx, const uint8_t *base, uint64_t 
     // split; at most n + target segments, and segment distances d stay below
     // 2^16 (the extents kernel's shift steps)
     const uint64_t target = std::min<uint64_t>(kSegPerWave * waves, 32768);
+    if (ctx->fused) {
+        // one launch (crc_ranges_fused_kernel): the plan inside every
+        // workgroup; extents shared by workgroups finish through two
+        // zero-at-rest words each (counter, XOR) that the kernel leaves zero
+        static_assert(kFusedMaxExtents == (uint64_t)kSegPlanThreads * kSegPlanPerThread, "one extent limit");
+        const uint32_t grid = (uint32_t)ctx->num_cus;
+        Scratch sc(ctx, s, ctx->cnt_pool, true);
+        if (int rc = sc.get((size_t)kFusedMaxExtents * 8))
+            return rc;
+        uint32_t *cnt = static_cast<uint32_t *>(sc.p);
+        uint32_t *xacc = cnt + kFusedMaxExtents;
+        const uint64_t sh = (uintptr_t)base & 15;
+        const uint8_t *abase = base - sh;
+        const uint32_t *lens_or_null = offs ? lens : nullptr;
+        const uint32_t tgt = 1u << (31 - __builtin_clz((uint32_t)target)); // the kernel takes a power of two
+        hipLaunchKernelGGL((crc_ranges_fused_kernel<kExtRows, kNbuf, kAux, kFusedPrio, kFusedWaves>), dim3(grid),
+                           dim3(64 * kFusedWaves), 0, s, abase, n, offs, lens_or_null, sh, stride, len_const,
+                           ctx->d_lds_image[0], ctx->d_nib16, ctx->d_rowshift, out, ctx->d_zpow, tgt, kSegMinShift,
+                           cnt, xacc);
+        const int rc = herr(hipGetLastError());
+        const int frc = sc.release();
+        *used = true;
+        return rc ? rc : frc;
+    }
     const size_t off_shift = ((n + 1) * 4 + 255) / 256 * 256;
     const size_t off_sub = off_shift + (n + 255) / 256 * 256;
     Scratch sc(ctx, s);
@@ -831,6 +885,8 @@ int priskv_crc_ctx_create(int device, priskv_crc_ctx **out)
         c->prio = !(pe && !strcmp(pe, "0"));
         const char *be = getenv("PRISKV_CRC_BALANCE");
         c->balance = !(be && !strcmp(be, "0"));
+        const char *fe = getenv("PRISKV_CRC_FUSED");
+        c->fused = !(fe && !strcmp(fe, "0"));
         c->seg_max_extents = kSegMaxExtents;
         c->tile_min_bytes = kTileMinBytes;
         c->tile_bytes = kTileBytes;
@@ -893,7 +949,8 @@ int priskv_crc_ctx_create(int device, priskv_crc_ctx **out)
     {
         int ev_ok = 1; // without the events every call keeps its own alloc/free
         for (int i = 0; i < NPOOL; i++)
-            ev_ok = ev_ok && hipEventCreateWithFlags(&c->pool[i].ev, hipEventDisableTiming) == hipSuccess;
+            ev_ok = ev_ok && hipEventCreateWithFlags(&c->pool[i].ev, hipEventDisableTiming) == hipSuccess &&
+                    hipEventCreateWithFlags(&c->cnt_pool[i].ev, hipEventDisableTiming) == hipSuccess;
         const char *pe = getenv("PRISKV_CRC_SCRATCH_POOL");
         c->pool_ready = ev_ok && !(pe && !strcmp(pe, "0"));
     }
@@ -933,15 +990,16 @@ void priskv_crc_ctx_destroy(priskv_crc_ctx *c)
     (void)hipFree(c->d_rowshift);
     (void)hipFree(c->d_zpow);
     (void)hipFree(c->d_scrub);
-    for (int i = 0; i < NPOOL; i++) {
-        priskv_crc_pool_slot &q = c->pool[i];
-        if (q.used)
-            (void)hipEventSynchronize(q.ev);
-        if (q.p)
-            (void)hipFreeAsync(q.p, c->aux);
-        if (q.ev)
-            (void)hipEventDestroy(q.ev);
-    }
+    for (priskv_crc_pool_slot *slots : {c->pool, c->cnt_pool})
+        for (int i = 0; i < NPOOL; i++) {
+            priskv_crc_pool_slot &q = slots[i];
+            if (q.used)
+                (void)hipEventSynchronize(q.ev);
+            if (q.p)
+                (void)hipFreeAsync(q.p, c->aux);
+            if (q.ev)
+                (void)hipEventDestroy(q.ev);
+        }
     if (c->aux) {
         (void)hipStreamSynchronize(c->aux);
         (void)hipStreamDestroy(c->aux);

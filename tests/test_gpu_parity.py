@@ -1095,3 +1095,87 @@ def test_blocks_host_partially_registered(torch_cuda, ctx):
     finally:
         host_unregister(half)
     assert np.array_equal(got, O.crc32_blocks(host, bs, nthreads=8))
+
+
+@pytest.fixture(scope="module")
+def ctx_threelaunch(torch_cuda):
+    """Few extents through the three-launch segmented path (plan kernel,
+    extents kernel, reduce kernel): PRISKV_CRC_FUSED=0, read at creation."""
+    c = _ctx_env(PRISKV_CRC_FUSED=0, PRISKV_CRC_SEG_MAX_EXTENTS=16384)
+    yield c
+    c.close()
+
+
+@pytest.fixture(scope="module")
+def ctx_fused16k(torch_cuda):
+    c = _ctx_env(PRISKV_CRC_SEG_MAX_EXTENTS=16384)
+    yield c
+    c.close()
+
+
+_FUSED_CASES = [
+    [256 << 20],                                  # a lone huge value: every workgroup holds part of it
+    [(1 << 14) + 1],                              # two segments, the last one byte
+    [0],                                          # a lone empty extent
+    [0] * 300,                                    # only empty extents
+    [5 << 20, 0, 7, (3 << 20) + 1, 0],            # split and whole extents mixed
+    [1 << 20] * 32,
+    [(64 << 20) + 3] * 3 + [100] * 1000,          # few large among many small
+    [4096] * 4096,                                # small values: kept whole
+    [4100] * 8192,
+    [(1 << 14) * 37 + 11] * 700,                  # extents straddling wave and workgroup edges
+]
+
+
+@pytest.mark.parametrize("case", range(len(_FUSED_CASES) + 2))
+def test_fused_few_extents(torch_cuda, ctx_fused16k, ctx_threelaunch, case):
+    """The one-launch few-extents kernel (plan in LDS, per-extent counters,
+    last-arriver combine) equals the oracle and the three-launch path, at
+    ragged offsets on a 16-B-misaligned base, called repeatedly (the counters
+    it leaves must read zero for the next call) -- and the counters survive
+    alternating shapes."""
+    torch = torch_cuda
+    rng = np.random.default_rng(4242 + case)
+    if case < len(_FUSED_CASES):
+        lens = np.array(_FUSED_CASES[case], dtype=np.uint32)
+    elif case == len(_FUSED_CASES):
+        lens = rng.integers(0, 40000, 16384).astype(np.uint32)   # the extent limit
+        lens[rng.integers(0, 16384, 50)] = 0
+    else:
+        lens = rng.integers(0, 3 << 19, 257).astype(np.uint32)
+    n = int(lens.sum()) + 64 * len(lens) + 4096
+    t = _region(torch, ctx_fused16k, n + 3, SEED ^ (0xF5 + case), 1)
+    base = t[3:]                                  # 16-B misaligned base (shift 3)
+    offs, pos = [], 0
+    for ln in lens:
+        pos += int(rng.integers(0, 64))
+        offs.append(pos)
+        pos += int(ln)
+    o = np.array(offs, dtype=np.uint64)
+    d_o = torch.from_numpy(o.astype(np.int64)).cuda()
+    d_l = torch.from_numpy(lens.view(np.int32)).cuda()
+    want = O.crc32_ranges(base[:n].cpu().numpy(), o, lens)
+    for c in (ctx_fused16k, ctx_threelaunch):
+        for _ in range(3):
+            got = _u32(c.ranges_dev(base, d_o, d_l))
+            torch.cuda.synchronize()
+            assert np.array_equal(got, want), (case, np.nonzero(got != want)[0][:8])
+    # a different shape in between, then the same call again
+    small = _u32(ctx_fused16k.ranges_dev(base, d_o[:1], d_l[:1]))
+    torch.cuda.synchronize()
+    assert small[0] == want[0]
+    got = _u32(ctx_fused16k.ranges_dev(base, d_o, d_l))
+    torch.cuda.synchronize()
+    assert np.array_equal(got, want)
+
+
+@pytest.mark.parametrize("bs,nb", [((3 << 20) + 5, 3), (4100 * 64, 17), ((1 << 24) + 1, 1)])
+def test_fused_constant_length_blocks(torch_cuda, ctx, bs, nb):
+    """Blocks that are not whole 1 KiB rows (the extents path with one length
+    and a stride): few large ones take the fused kernel with no lengths array."""
+    torch = torch_cuda
+    t = _region(torch, ctx, bs * nb, SEED ^ 0xC0, 1)
+    got = _u32(ctx.blocks_dev(t, bs, nblocks=nb))
+    torch.cuda.synchronize()
+    want = O.crc32_blocks(t[: bs * nb].cpu().numpy(), bs, nthreads=8)
+    assert np.array_equal(got, want), (bs, nb)
