@@ -560,47 +560,66 @@ constexpr uint32_t kSegMinLen = 64u << 10;
 // mode 3, 4096 small values 7.6 vs 7.7 us (profiles/r02/fused/ktrace_shapes_*)
 constexpr int kFusedPrio = 0;
 
+// one segment size per call (crc_seg_plan_kernel / the fused kernel): about
+// kSegPerWave full segments per resident wave, so the count split of
+// segments is a byte split; at most n + target segments, and segment
+// distances stay below 2^16
+uint64_t seg_target(const priskv_crc_ctx *ctx)
+{
+    const uint64_t waves = (uint64_t)ctx->num_cus * kExtWgPerCu * kExtWaves;
+    return std::min<uint64_t>(kSegPerWave * waves, 32768);
+}
+
+// does an extents call take the segmented path?  max_len: the longest
+// extent when the host knows it (0: device-resident lengths)
+bool extents_segmented(const priskv_crc_ctx *ctx, uint64_t n, uint64_t max_len)
+{
+    const uint64_t waves = (uint64_t)ctx->num_cus * kExtWgPerCu * kExtWaves;
+    if (!ctx->segment || n == 0 || n > (uint64_t)kSegPlanThreads * kSegPlanPerThread)
+        return false;
+    return max_len ? !(max_len < kSegMinLen || balanced(n, waves)) : n <= ctx->seg_max_extents;
+}
+
+// the fused few-extents kernel, one launch (n <= kFusedMaxExtents): the plan
+// inside every workgroup; extents shared by workgroups finish through two
+// zero-at-rest words each (counter, XOR) that the kernel leaves zero
+int launch_fused(const priskv_crc_ctx *ctx, const uint8_t *base, uint64_t n, const uint64_t *offs,
+                 const uint32_t *lens, uint64_t stride, uint32_t len_const, uint32_t *out, hipStream_t s)
+{
+    static_assert(kFusedMaxExtents == (uint64_t)kSegPlanThreads * kSegPlanPerThread, "one extent limit");
+    if (n == 0 || n > kFusedMaxExtents)
+        return -EINVAL;
+    const uint32_t grid = (uint32_t)ctx->num_cus;
+    Scratch sc(ctx, s, ctx->cnt_pool, true);
+    if (int rc = sc.get((size_t)kFusedMaxExtents * 8))
+        return rc;
+    uint32_t *cnt = static_cast<uint32_t *>(sc.p);
+    uint32_t *xacc = cnt + kFusedMaxExtents;
+    const uint64_t sh = (uintptr_t)base & 15;
+    const uint8_t *abase = base - sh;
+    const uint32_t *lens_or_null = offs ? lens : nullptr;
+    const uint32_t tgt = 1u << (31 - __builtin_clz((uint32_t)seg_target(ctx))); // the kernel takes a power of two
+    hipLaunchKernelGGL((crc_ranges_fused_kernel<kExtRows, kNbuf, kAux, kFusedPrio, kFusedWaves>), dim3(grid),
+                       dim3(64 * kFusedWaves), 0, s, abase, n, offs, lens_or_null, sh, stride, len_const,
+                       ctx->d_lds_image[0], ctx->d_nib16, ctx->d_rowshift, out, ctx->d_zpow, tgt, kSegMinShift, cnt,
+                       xacc);
+    const int rc = herr(hipGetLastError());
+    const int frc = sc.release();
+    return rc ? rc : frc;
+}
+
 int launch_extents_seg(const priskv_crc_ctx *ctx, const uint8_t *base, uint64_t n, const uint64_t *offs,
                        const uint32_t *lens, uint64_t stride, uint32_t len_const, uint32_t *out, hipStream_t s,
                        uint64_t max_len, bool *used)
 {
-    const uint64_t waves = (uint64_t)ctx->num_cus * kExtWgPerCu * kExtWaves;
     *used = false;
-    if (!offs)
-        max_len = len_const;
-    if (!ctx->segment || n == 0 || n > (uint64_t)kSegPlanThreads * kSegPlanPerThread)
+    if (!extents_segmented(ctx, n, offs ? max_len : len_const))
         return 0;
-    if (max_len ? (max_len < kSegMinLen || balanced(n, waves)) : n > ctx->seg_max_extents)
-        return 0;
-    // one segment size per call (crc_seg_plan_kernel): about kSegPerWave full
-    // segments per resident wave, so the count split of segments is a byte
-    // split; at most n + target segments, and segment distances d stay below
-    // 2^16 (the extents kernel's shift steps)
-    const uint64_t target = std::min<uint64_t>(kSegPerWave * waves, 32768);
-    if (ctx->fused) {
-        // one launch (crc_ranges_fused_kernel): the plan inside every
-        // workgroup; extents shared by workgroups finish through two
-        // zero-at-rest words each (counter, XOR) that the kernel leaves zero
-        static_assert(kFusedMaxExtents == (uint64_t)kSegPlanThreads * kSegPlanPerThread, "one extent limit");
-        const uint32_t grid = (uint32_t)ctx->num_cus;
-        Scratch sc(ctx, s, ctx->cnt_pool, true);
-        if (int rc = sc.get((size_t)kFusedMaxExtents * 8))
-            return rc;
-        uint32_t *cnt = static_cast<uint32_t *>(sc.p);
-        uint32_t *xacc = cnt + kFusedMaxExtents;
-        const uint64_t sh = (uintptr_t)base & 15;
-        const uint8_t *abase = base - sh;
-        const uint32_t *lens_or_null = offs ? lens : nullptr;
-        const uint32_t tgt = 1u << (31 - __builtin_clz((uint32_t)target)); // the kernel takes a power of two
-        hipLaunchKernelGGL((crc_ranges_fused_kernel<kExtRows, kNbuf, kAux, kFusedPrio, kFusedWaves>), dim3(grid),
-                           dim3(64 * kFusedWaves), 0, s, abase, n, offs, lens_or_null, sh, stride, len_const,
-                           ctx->d_lds_image[0], ctx->d_nib16, ctx->d_rowshift, out, ctx->d_zpow, tgt, kSegMinShift,
-                           cnt, xacc);
-        const int rc = herr(hipGetLastError());
-        const int frc = sc.release();
-        *used = true;
-        return rc ? rc : frc;
-    }
+    *used = true;
+    if (ctx->fused)
+        return launch_fused(ctx, base, n, offs, lens, stride, len_const, out, s);
+    // PRISKV_CRC_FUSED=0: plan kernel -> extents kernel -> reduce kernel
+    const uint64_t target = seg_target(ctx);
     const size_t off_shift = ((n + 1) * 4 + 255) / 256 * 256;
     const size_t off_sub = off_shift + (n + 255) / 256 * 256;
     Scratch sc(ctx, s);
@@ -629,12 +648,20 @@ int launch_extents_seg(const priskv_crc_ctx *ctx, const uint8_t *base, uint64_t 
     return rc ? rc : frc;
 }
 
+// few large blocks through the fused kernel up to the wave-planned size (1024 x
+// 1 MiB is 3 % faster through rows + combine)
+bool fused_blocks(const priskv_crc_ctx *ctx, uint64_t nblocks) { return ctx->fused && nblocks <= kFusedWavePlan; }
+
 int launch_rows(const priskv_crc_ctx *ctx, const uint8_t *base, uint64_t nblocks, uint32_t bs, uint32_t *out,
                 hipStream_t s)
 {
     const uint32_t S = segments_for(ctx, nblocks, bs);
     if (S == 1)
         return launch_rows_plain(ctx, base, nblocks, bs, out, s);
+    // few large blocks: the fused few-extents kernel in one launch (1 x 256 MiB
+    // 50 us against 55-57 for rows + combine, 1024 x 1 MiB level: DESIGN §4)
+    if (fused_blocks(ctx, nblocks))
+        return launch_fused(ctx, base, nblocks, nullptr, nullptr, bs, bs, out, s);
     Scratch sc(ctx, s); // pooled, ordered by events: concurrent calls never share a slot
     if (int rc = sc.get(nblocks * S * sizeof(uint32_t)))
         return rc;
@@ -819,7 +846,10 @@ int priskv_crc32_blocks_plan(const priskv_crc_ctx *ctx, const void *d_base, uint
         return -EINVAL;
     const int path = choose_path(d_base, block_size);
     int w = 0;
-    if (path == PATH_ROWS) {
+    const char *fused_name = "crc_ranges_fused_kernel (few large values: segments, one launch)";
+    if (path == PATH_ROWS && segments_for(ctx, nblocks, block_size) > 1 && fused_blocks(ctx, nblocks)) {
+        w = snprintf(buf, len, "%s", fused_name);
+    } else if (path == PATH_ROWS) {
         const uint32_t S = segments_for(ctx, nblocks, block_size);
         const uint32_t bs = block_size / S;
         const int p = plan_for(bs);
@@ -843,7 +873,11 @@ int priskv_crc32_blocks_plan(const priskv_crc_ctx *ctx, const void *d_base, uint
     } else if (path == PATH_SMALL) {
         w = snprintf(buf, len, "crc_small_kernel<G=%u>", block_size / 16);
     } else if (path == PATH_EXTENTS) {
-        w = snprintf(buf, len, "crc_ranges_kernel (extents)");
+        const bool seg = extents_segmented(ctx, nblocks, block_size);
+        w = snprintf(buf, len, "%s", !seg ? "crc_ranges_kernel (extents)"
+                                          : (ctx->fused ? fused_name
+                                                        : "crc_seg_plan_kernel + crc_ranges_kernel (segments) + "
+                                                          "crc_seg_reduce_kernel"));
     } else {
         w = snprintf(buf, len, "crc_generic_kernel");
     }

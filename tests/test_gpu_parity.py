@@ -341,15 +341,17 @@ def test_ranges_chunk_boundaries(torch_cuda, any_ctx):
 @pytest.mark.parametrize("bs,nb", [(1 << 20, 1), (1 << 20, 3), (1 << 20, 100), (2 << 20, 5), (4 << 20, 2),
                                    (48 << 10, 7), (3 << 20, 1), (1025 << 10, 3), (96 << 10, 1000),
                                    (64 << 20, 1), (48 << 20, 2), (3 << 24, 1)])
-def test_segmented_large_blocks(torch_cuda, ctx, bs, nb):
-    """Batches of few large blocks are hashed as equal segments and combined
+def test_segmented_large_blocks(torch_cuda, ctx, ctx_threelaunch, bs, nb):
+    """Batches of few large blocks: the fused few-extents kernel (default) and,
+    with PRISKV_CRC_FUSED=0, equal segments through the rows kernel combined
     with Z_seg (crc_combine_segments_kernel); results must not change."""
     torch = torch_cuda
     t = _region(torch, ctx, bs * nb, SEED ^ 0x51, nb)
-    out = ctx.blocks_dev(t, bs, nblocks=nb)
-    torch.cuda.synchronize()
     want = O.crc32_blocks(t[: bs * nb].cpu().numpy(), bs, nthreads=8)
-    assert np.array_equal(_u32(out), want), (bs, nb)
+    for c in (ctx, ctx_threelaunch):
+        out = c.blocks_dev(t, bs, nblocks=nb)
+        torch.cuda.synchronize()
+        assert np.array_equal(_u32(out), want), (bs, nb)
 
 
 @pytest.mark.parametrize("lens", [[64 << 20], [(1 << 20) + 5, 16 << 20, 0, 17], [1 << 20] * 32,
@@ -993,7 +995,11 @@ def test_blocks_plan_strings(torch_cuda, ctx):
     assert ctx.blocks_plan(base, 1 << 16, 65536).startswith("crc_rows_kernel<G=64,CH=4,NBUF=2,nt,progress-priority 1")
     # the 128 GiB shard of BASELINE configs[3] runs in block-cyclic 1 MiB tiles
     assert "block-cyclic tiles of 16 groups" in ctx.blocks_plan(base, 1 << 21, 65536)
-    assert "segments" in ctx.blocks_plan(base, 1, 1 << 20)
+    assert ctx.blocks_plan(base, 1, 1 << 20).startswith("crc_ranges_fused_kernel")  # few large blocks
+    assert ctx.blocks_plan(base + 1, 3, (3 << 20) + 5).startswith("crc_ranges_fused_kernel")
+    assert ctx.blocks_plan(base, 20000, 1 << 20).startswith("crc_rows_kernel")  # balanced: whole blocks
+    # more than 64 unbalanced large blocks: rows kernel on segments + combine
+    assert "crc_combine_segments_kernel" in ctx.blocks_plan(base, 1000, 1 << 20)
     assert ctx.blocks_plan(base, 100, 256) == "crc_small_kernel<G=16>"
     assert ctx.blocks_plan(base + 1, 100, 4096) == "crc_ranges_kernel (extents)"
     assert ctx.blocks_plan(base, 100, 100) == "crc_generic_kernel"

@@ -28,12 +28,13 @@ if "--noseg" in sys.argv:
     del os.environ["PRISKV_CRC_SEG_MAX_EXTENTS"]
 ctx = ctxs[0][1]
 s = torch.cuda.Stream()
-t = torch.empty(512 << 20, dtype=torch.uint8, device="cuda")
+t = torch.empty(1 << 30, dtype=torch.uint8, device="cuda")
 ctx.fill_splitmix(t, 7, 0)
 for name, n, ln, stride in (("1x256MiB", 1, 256 << 20, 0), ("32x1MiB", 32, 1 << 20, (1 << 20) + 4096),
                             ("4096x4KiB-100", 4096, 4096 - 100, 4096), ("4096x64KiB", 4096, 65536, 65536),
                             ("16384x16KiB", 16384, 16384, 16384), ("1x4KiB", 1, 4096, 0), ("64x4KiB", 64, 4096, 4096),
-                            ("65x4KiB", 65, 4096, 4096)):
+                            ("65x4KiB", 65, 4096, 4096), ("4x64MiB", 4, 64 << 20, 64 << 20),
+                            ("16x16MiB", 16, 16 << 20, 16 << 20), ("1024x1MiB", 1024, 1 << 20, 1 << 20)):
     offs = torch.arange(n, dtype=torch.int64, device="cuda") * stride
     lens = torch.full((n,), ln, dtype=torch.int32, device="cuda")
     out = torch.empty(n, dtype=torch.int32, device="cuda")
@@ -51,7 +52,8 @@ for name, n, ln, stride in (("1x256MiB", 1, 256 << 20, 0), ("32x1MiB", 32, 1 << 
         print(json.dumps({"case": name, "path": path, "us_per_call": round(us, 2),
                           "TBs": round(n * ln / (us * 1e-6) / 1e12, 3)}), flush=True)
 if "--blocks" in sys.argv:  # the rows machinery on 256 MiB: one block (segments + combine), 16 KiB and 4 KiB blocks
-    for bs, nb in ((256 << 20, 1), (16384, 16384), (4096, 65536), (65536, 4096), (1 << 20, 256), (1 << 17, 2048)):
+    for bs, nb in ((256 << 20, 1), (64 << 20, 4), (16 << 20, 16), (1 << 20, 1024), (16384, 16384), (4096, 65536),
+                   (65536, 4096)):
         out = torch.empty(nb, dtype=torch.int32, device="cuda")
         with torch.cuda.stream(s):
             for _ in range(30):
