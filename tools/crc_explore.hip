@@ -530,6 +530,13 @@ int main(int argc, char **argv)
     all.push_back(NIB_VARIANT_W(32, 8, 2, 2, 1, 2 | 768, 31, 29));
     all.push_back(NIB_VARIANT_W(32, 8, 2, 2, 1, 2 | 768 | 8, 31, 29));
     all.push_back(PROD_VARIANT(64, 4, 3, 2 | 32 | 768, 31, 29));
+    all.push_back(PROD_VARIANT(64, 4, 3, 2 | 32 | 768, 32, 28));
+    all.push_back(PROD_VARIANT(64, 4, 3, 2 | 32 | 768, 33, 27));
+    all.push_back(PROD_VARIANT(64, 4, 3, 2 | 32 | 768, 34, 26));
+    all.push_back(PROD_VARIANT(64, 4, 3, 2 | 32 | 768, 36, 24));
+    all.push_back(PROD_VARIANT(64, 4, 3, 2 | 32 | 768, 1, 1));
+    all.push_back(NIB_VARIANT_W(64, 4, 3, 2, 1, 2 | 768 | 8, 33, 27));
+    all.push_back(NIB_VARIANT_W(64, 4, 3, 2, 1, 2 | 768 | 8, 34, 26));
     all.push_back(CRC_VARIANT_W(64, 4, 2, 2, 1, 256 | 8192, 0, 0));
     all.push_back(CRC_VARIANT_W(64, 4, 2, 2, 1, 256 | 8192 | 16384, 0, 0));
     all.push_back(CRC_VARIANT_W(64, 4, 2, 2, 1, 256 | 8192 | 32768, 0, 0));
