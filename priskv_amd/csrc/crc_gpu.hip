@@ -705,17 +705,23 @@ int launch_rows_plain(const priskv_crc_ctx *ctx, const uint8_t *base, uint64_t n
 // 8-wave workgroups per CU (PRISKV_CRC_PRIO=0)
 constexpr int kSmallOptPrio = 1 | (1 << 8) | 1024;
 
+// Chunk shape: 4 rows per chunk with 3 chunks in the register pipeline
+// (was 2): +1.3-2.8 % for G >= 2 and +2.2-2.8 % for G = 1, 1 GiB per call
+// (profiles/r02/small/).  8 rows 3 deep was 1.5 % faster still at G = 1,
+// but at 182 VGPRs it halves the resident waves.
+constexpr int kSmallCh = 4, kSmallNbuf = 3, kSmallCh1 = 4, kSmallNbuf1 = 3;
+
 template <int G>
 const void *small_fn_g(bool prio)
 {
-    return prio ? reinterpret_cast<const void *>(&crc_small_kernel<G, kSmallOptPrio>)
+    return prio ? reinterpret_cast<const void *>(&crc_small_kernel<G, kSmallOptPrio, kSmallCh, kSmallNbuf>)
                 : reinterpret_cast<const void *>(&crc_small_kernel<G, 1>);
 }
 
 const void *small_fn(int gl, bool prio)
 {
     switch (gl) {
-    case 0: return reinterpret_cast<const void *>(&crc_small_kernel<1, 0>);
+    case 0: return reinterpret_cast<const void *>(&crc_small_kernel<1, 0, kSmallCh1, kSmallNbuf1>);
     case 1: return small_fn_g<2>(prio);
     case 2: return small_fn_g<4>(prio);
     case 3: return small_fn_g<8>(prio);
@@ -741,7 +747,8 @@ int launch_blocks(const priskv_crc_ctx *ctx, const uint8_t *base, uint64_t nbloc
             const bool prio = gl && ctx->prio;
             const int waves = prio ? 2 * kWaves : kWaves;
             const uint64_t cap = prio ? (uint64_t)ctx->num_cus : (uint64_t)ctx->max_wgs;
-            const uint64_t want = (nrows + 4 * waves - 1) / (4 * waves);
+            const uint64_t chw = (uint64_t)(gl == 0 ? kSmallCh1 : prio ? kSmallCh : 4) * waves; // rows per wave-chunk
+            const uint64_t want = (nrows + chw - 1) / chw;
             const uint32_t grid = (uint32_t)(want < cap ? want : cap);
             void *args[] = {(void *)&base, (void *)&nrows, (void *)&img, (void *)&fold, (void *)&out};
             if (int rc = herr(hipLaunchKernel(small_fn(gl, prio), dim3(grid), dim3(64 * waves), args, 0, s)))
