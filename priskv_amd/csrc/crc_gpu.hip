@@ -200,8 +200,8 @@ struct Scratch {
                     q.size = 0;
                     if (!rc && !(rc = herr(hipMallocAsync(&q.p, cap, s))))
                         q.size = cap;
-                    if (!rc && zero)
-                        rc = zero_fill(q.p, cap);
+                    if (!rc && zero && (rc = zero_fill(q.p, cap)))
+                        q.size = 0; // not known zero: the next user reallocates (and frees q.p)
                 }
                 if (rc) {
                     pthread_mutex_lock(&ctx->pool_lock);
