@@ -1130,6 +1130,8 @@ _FUSED_CASES = [
     [4096] * 4096,                                # small values: kept whole
     [4100] * 8192,
     [(1 << 14) * 37 + 11] * 700,                  # extents straddling wave and workgroup edges
+    [(1 << 20) + 1] * 64,                         # the largest wave-planned call, split
+    [(1 << 20) + 1] * 65,                         # the smallest workgroup-planned one
 ]
 
 
@@ -1185,3 +1187,36 @@ def test_fused_constant_length_blocks(torch_cuda, ctx, bs, nb):
     torch.cuda.synchronize()
     want = O.crc32_blocks(t[: bs * nb].cpu().numpy(), bs, nthreads=8)
     assert np.array_equal(got, want), (bs, nb)
+
+
+@pytest.mark.parametrize("kind", ["block_3GiB", "extent_2GiB_plus", "extent_near_4GiB"])
+def test_fused_single_value_beyond_2GiB(torch_cuda, ctx, kind):
+    """One value of 2-4 GiB through the fused kernel: a few-large-blocks call
+    (3 GiB block), and ranges at offsets beyond 4 GiB with lengths past 2^31
+    and up to 2^32 - 5 (u32 lengths, segment and shift arithmetic at the top
+    of their range)."""
+    torch = torch_cuda
+    if kind == "block_3GiB":
+        bs = 3 << 30
+        t = _region(torch, ctx, bs, SEED ^ 0x3, 0)
+        assert ctx.blocks_plan(t.data_ptr(), 1, bs).startswith("crc_ranges_fused_kernel")
+        got = _u32(ctx.blocks_dev(t, bs, nblocks=1))
+        torch.cuda.synchronize()
+        want = O.crc32_blocks(t[:bs].cpu().numpy(), bs, nthreads=8)
+        assert np.array_equal(got, want)
+        del t
+    else:
+        ln = (2 << 30) + 4096 + 3 if kind == "extent_2GiB_plus" else (1 << 32) - 5
+        off = (4 << 30) + 7
+        n_bytes = off + ln + 64
+        t = _region(torch, ctx, n_bytes, SEED ^ 0x4, 0)
+        offs = np.array([off, 5], dtype=np.uint64)
+        lens = np.array([ln, 100], dtype=np.uint32)
+        got = _u32(ctx.ranges_dev(t, torch.from_numpy(offs.astype(np.int64)).cuda(),
+                                  torch.from_numpy(lens.view(np.int32)).cuda()))
+        torch.cuda.synchronize()
+        host = t[: off + ln].cpu().numpy()
+        want = O.crc32_ranges(host, offs, lens)
+        assert np.array_equal(got, want), (kind, got, want)
+        del t, host
+    torch.cuda.empty_cache()
