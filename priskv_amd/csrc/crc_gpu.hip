@@ -103,6 +103,11 @@ struct priskv_crc_ctx {
     // allocated; the kernel leaves the counters zero; guarded by pool_lock)
     mutable priskv_crc_pool_slot cnt_pool[NPOOL];
     int fused;                 // few extents in one launch (PRISKV_CRC_FUSED=0: the three-launch path)
+    int stride;                // odd block sizes / unaligned bases take crc_stride_kernel (PRISKV_CRC_STRIDE=0: the
+                               // extents / generic kernels, as in round 2)
+    int stride_g;              // PRISKV_CRC_STRIDE_G: force the stride kernel's G (0 = cost model; tuning)
+    int stride_shape;          // PRISKV_CRC_STRIDE_SHAPE: chunk shape variant (tuning)
+    int stride_wgs;            // PRISKV_CRC_STRIDE_WGS: workgroups per CU (tuning)
 };
 
 namespace {
@@ -241,15 +246,19 @@ struct Scratch {
 
 inline bool is_pow2(uint64_t v) { return v && !(v & (v - 1)); }
 
-enum Path { PATH_ROWS = 1, PATH_EXTENTS = 2, PATH_SMALL = 3, PATH_GENERIC = 4 };
+enum Path { PATH_ROWS = 1, PATH_EXTENTS = 2, PATH_SMALL = 3, PATH_GENERIC = 4, PATH_STRIDE = 5 };
 
-int choose_path(const void *d_base, uint32_t block_size)
+// stride = 0: round 2's dispatch of odd sizes / unaligned bases (extents from
+// 1 KiB, generic below)
+int choose_path(const void *d_base, uint32_t block_size, int stride = 1)
 {
     const bool aligned = ((uintptr_t)d_base & 15) == 0;
     if (aligned && block_size % PRV_ROW_BYTES == 0)
         return PATH_ROWS;
     if (aligned && is_pow2(block_size) && block_size >= 16 && block_size <= 512)
         return PATH_SMALL;
+    if (stride && block_size >= 16)
+        return PATH_STRIDE;
     if (block_size >= PRV_ROW_BYTES)
         return PATH_EXTENTS;
     return PATH_GENERIC;
@@ -730,12 +739,110 @@ const void *small_fn(int gl, bool prio)
     }
 }
 
+// ---- uniform-stride kernel (odd block sizes, unaligned bases) ------------------
+// G lanes per block with R = ceil(B / 16G) rows; G < 16 only for R = 1 (the
+// set-B row jump exists for G = 16, 32, 64).  Cost model: lane-rows per block
+// plus half a row for the fold, G * (R + 1/2), so the least padding F = R*16G
+// - B and the fewest folds per byte.  4100 B -> G16 x 17 rows, 100 B -> G8 x
+// 1, 1000 B -> G16 x 4.
+struct StridePlan {
+    int G;
+    uint32_t R;
+};
+
+StridePlan stride_plan(const priskv_crc_ctx *ctx, uint32_t bs)
+{
+    StridePlan best{0, 0};
+    uint64_t bc = ~0ull;
+    for (int pass = 0; pass < 2 && !best.G; pass++)
+        for (int G = 2; G <= 64; G *= 2) {
+            const uint32_t RB = 16u * (uint32_t)G, R = (uint32_t)(((uint64_t)bs + RB - 1) / RB);
+            if ((G < 16 && R > 1) || (pass == 0 && ctx->stride_g && G != ctx->stride_g))
+                continue;
+            const uint64_t cost = (uint64_t)G * (2ull * R + 1);
+            if (cost < bc) {
+                bc = cost;
+                best = {G, R};
+            }
+        }
+    return best;
+}
+
+// chunk shapes: 0 = the default, 1-3 tuning variants (PRISKV_CRC_STRIDE_SHAPE)
+template <int G>
+const void *stride_fn_g(int shape)
+{
+    constexpr bool small = G < 16;
+    switch (shape) {
+    case 1: return reinterpret_cast<const void *>(&crc_stride_kernel<G, 4, small ? 2 : 3, kAux>);
+    case 2: return reinterpret_cast<const void *>(&crc_stride_kernel<G, 2, 4, kAux>);
+    case 3: return reinterpret_cast<const void *>(&crc_stride_kernel<G, 8, 2, kAux>);
+    default: return reinterpret_cast<const void *>(&crc_stride_kernel<G, 4, small ? 3 : 2, kAux>);
+    }
+}
+
+const void *stride_fn(int G, int shape)
+{
+    switch (G) {
+    case 2: return stride_fn_g<2>(shape);
+    case 4: return stride_fn_g<4>(shape);
+    case 8: return stride_fn_g<8>(shape);
+    case 16: return stride_fn_g<16>(shape);
+    case 32: return stride_fn_g<32>(shape);
+    default: return stride_fn_g<64>(shape);
+    }
+}
+
+// Few large odd blocks: the stride kernel splits groups statically like the
+// rows kernel, so an unbalanced handful of big blocks goes to the fused
+// few-extents kernel, which cuts them into segments (as launch_rows does)
+bool stride_segmented(const priskv_crc_ctx *ctx, const StridePlan &P, uint64_t nblocks, uint32_t bs)
+{
+    const uint64_t NB = 64 / (uint64_t)P.G;
+    const uint64_t waves = (uint64_t)ctx->num_cus * ctx->stride_wgs * kWaves;
+    return ctx->segment && ctx->fused && bs >= kSegMinLen && nblocks <= kFusedMaxExtents &&
+           !balanced((nblocks + NB - 1) / NB, waves);
+}
+
+int launch_stride(const priskv_crc_ctx *ctx, const uint8_t *base, uint64_t nblocks, uint32_t bs, uint32_t *out,
+                  hipStream_t s)
+{
+    const StridePlan P = stride_plan(ctx, bs);
+    if (stride_segmented(ctx, P, nblocks, bs))
+        return launch_fused(ctx, base, nblocks, nullptr, nullptr, bs, bs, out, s);
+    const uint64_t NB = 64 / (uint64_t)P.G;
+    const uint64_t max_wgs = (uint64_t)ctx->num_cus * ctx->stride_wgs;
+    const uint64_t ngroups = (nblocks + NB - 1) / NB;
+    // the kernel counts a wave's rows in 32 bits: cap groups per launch
+    const uint64_t cap = max_wgs * kWaves * ((1ull << 31) / P.R - 1);
+    const uint32_t *img = ctx->d_lds_image[P.G == 64 ? 0 : (P.G == 32 ? 1 : 2)]; // set B unused for G < 16 (R = 1)
+    const uint32_t *nib = ctx->d_nibrep[log2u((uint32_t)P.G)];
+    const void *fn = stride_fn(P.G, ctx->stride_shape);
+    uint32_t R = P.R;
+    for (uint64_t done = 0; done < ngroups;) {
+        const uint64_t n = ngroups - done < cap ? ngroups - done : cap;
+        const uint64_t want = (n + kWaves - 1) / kWaves;
+        const uint32_t grid = (uint32_t)(want < max_wgs ? want : max_wgs);
+        const uint8_t *b = base + done * NB * bs;
+        uint64_t nb = nblocks - done * NB;
+        nb = nb < n * NB ? nb : n * NB;
+        uint32_t *o = out + done * NB;
+        void *args[] = {(void *)&b, (void *)&nb, (void *)&bs, (void *)&R, (void *)&img, (void *)&nib, (void *)&o};
+        if (int rc = herr(hipLaunchKernel(fn, dim3(grid), dim3(kThreads), args, 0, s)))
+            return rc;
+        done += n;
+    }
+    return 0;
+}
+
 int launch_blocks(const priskv_crc_ctx *ctx, const uint8_t *base, uint64_t nblocks, uint32_t bs,
                   uint32_t *out, hipStream_t s)
 {
-    const int path = choose_path(base, bs);
+    const int path = choose_path(base, bs, ctx->stride);
     if (path == PATH_ROWS)
         return launch_rows(ctx, base, nblocks, bs, out, s);
+    if (path == PATH_STRIDE)
+        return launch_stride(ctx, base, nblocks, bs, out, s);
     if (path == PATH_SMALL) {
         const int gl = log2u(bs / 16); // G = 1 << gl
         const uint64_t per = 1024 / bs; // blocks per row
@@ -851,10 +958,22 @@ int priskv_crc32_blocks_plan(const priskv_crc_ctx *ctx, const void *d_base, uint
 {
     if (!ctx || block_size == 0 || !buf || len == 0)
         return -EINVAL;
-    const int path = choose_path(d_base, block_size);
+    const int path = choose_path(d_base, block_size, ctx->stride);
     int w = 0;
     const char *fused_name = "crc_ranges_fused_kernel (few large values: segments, one launch)";
-    if (path == PATH_ROWS && segments_for(ctx, nblocks, block_size) > 1 && fused_blocks(ctx, nblocks)) {
+    if (path == PATH_STRIDE) {
+        const StridePlan P = stride_plan(ctx, block_size);
+        if (stride_segmented(ctx, P, nblocks, block_size)) {
+            w = snprintf(buf, len, "%s", fused_name);
+        } else {
+            static const int kShapeCh[4][2] = {{4, 0}, {4, 1}, {2, 4}, {8, 2}}; // CH, NBUF (0/1: 3/2 or 2/3 by G)
+            const int sh = ctx->stride_shape;
+            const int ch = kShapeCh[sh][0];
+            const int nbuf = sh == 0 ? (P.G < 16 ? 3 : 2) : (sh == 1 ? (P.G < 16 ? 2 : 3) : kShapeCh[sh][1]);
+            w = snprintf(buf, len, "crc_stride_kernel<G=%d,CH=%d,NBUF=%d,nt> (%u rows of %u B per block, %u B in front)",
+                         P.G, ch, nbuf, P.R, 16u * P.G, P.R * 16u * P.G - block_size);
+        }
+    } else if (path == PATH_ROWS && segments_for(ctx, nblocks, block_size) > 1 && fused_blocks(ctx, nblocks)) {
         w = snprintf(buf, len, "%s", fused_name);
     } else if (path == PATH_ROWS) {
         const uint32_t S = segments_for(ctx, nblocks, block_size);
@@ -928,6 +1047,19 @@ int priskv_crc_ctx_create(int device, priskv_crc_ctx **out)
         c->balance = !(be && !strcmp(be, "0"));
         const char *fe = getenv("PRISKV_CRC_FUSED");
         c->fused = !(fe && !strcmp(fe, "0"));
+        const char *se = getenv("PRISKV_CRC_STRIDE");
+        c->stride = !(se && !strcmp(se, "0"));
+        c->stride_g = 0;
+        if (const char *m = getenv("PRISKV_CRC_STRIDE_G")) {
+            const int v = atoi(m);
+            c->stride_g = (v >= 2 && v <= 64 && !(v & (v - 1))) ? v : 0;
+        }
+        c->stride_shape = 0;
+        if (const char *m = getenv("PRISKV_CRC_STRIDE_SHAPE"))
+            c->stride_shape = atoi(m) & 3;
+        c->stride_wgs = 1;
+        if (const char *m = getenv("PRISKV_CRC_STRIDE_WGS"))
+            c->stride_wgs = atoi(m) == 2 ? 2 : 1;
         c->seg_max_extents = kSegMaxExtents;
         c->tile_min_bytes = kTileMinBytes;
         c->tile_bytes = kTileBytes;

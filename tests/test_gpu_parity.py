@@ -1001,8 +1001,16 @@ def test_blocks_plan_strings(torch_cuda, ctx):
     # more than 64 unbalanced large blocks: rows kernel on segments + combine
     assert "crc_combine_segments_kernel" in ctx.blocks_plan(base, 1000, 1 << 20)
     assert ctx.blocks_plan(base, 100, 256) == "crc_small_kernel<G=16>"
-    assert ctx.blocks_plan(base + 1, 100, 4096) == "crc_ranges_kernel (extents)"
-    assert ctx.blocks_plan(base, 100, 100) == "crc_generic_kernel"
+    # odd sizes and unaligned bases: the uniform-stride kernel
+    assert ctx.blocks_plan(base + 1, 100, 4096).startswith("crc_stride_kernel<G=16,CH=4,NBUF=2,nt> (16 rows of 256 B")
+    assert ctx.blocks_plan(base, 100, 4100).startswith("crc_stride_kernel<G=16,CH=4,NBUF=2,nt> (17 rows of 256 B "
+                                                       "per block, 252 B in front)")
+    assert ctx.blocks_plan(base, 100, 100).startswith("crc_stride_kernel<G=8,CH=4,NBUF=3,nt> (1 rows of 128 B")
+    assert ctx.blocks_plan(base, 100, 15) == "crc_generic_kernel"
+    off = _ctx_env(PRISKV_CRC_STRIDE="0")  # round 2's dispatch
+    assert off.blocks_plan(base + 1, 100, 4096) == "crc_ranges_kernel (extents)"
+    assert off.blocks_plan(base, 100, 100) == "crc_generic_kernel"
+    off.close()
 
 
 def test_ranges_host_concurrent_temporary_registration(torch_cuda):
@@ -1219,4 +1227,84 @@ def test_fused_single_value_beyond_2GiB(torch_cuda, ctx, kind):
         want = O.crc32_ranges(host, offs, lens)
         assert np.array_equal(got, want), (kind, got, want)
         del t, host
+    torch.cuda.empty_cache()
+
+
+# (G, block sizes the forced G can take): G < 16 only with one row per block
+_STRIDE_SIZES = {2: [16, 17, 23, 32], 4: [33, 48, 50, 64], 8: [65, 100, 127, 128],
+                 16: [129, 255, 257, 1000, 4100, 65537], 32: [257, 511, 1000, 4097, 12345],
+                 64: [513, 1023, 1025, 3000, 100003]}
+
+
+@pytest.mark.parametrize("G", sorted(_STRIDE_SIZES))
+def test_stride_kernel_every_g_and_shape(torch_cuda, G):
+    """crc_stride_kernel (odd block sizes, unaligned bases) for every lane
+    count G (forced, PRISKV_CRC_STRIDE_G) and chunk shape
+    (PRISKV_CRC_STRIDE_SHAPE 0-3): the oracle's CRCs at base misalignments 0,
+    3 and 4, for batches of 1 block, a ragged last group, and several groups
+    per wave with a ragged end."""
+    torch = torch_cuda
+    ctxs = [_ctx_env(PRISKV_CRC_STRIDE_G=G, PRISKV_CRC_STRIDE_SHAPE=sh) for sh in range(4)]
+    per = 64 // G
+    rng = np.random.default_rng(G)
+    try:
+        for bs in _STRIDE_SIZES[G]:
+            big = max(per + 1, min((24 << 20) // bs, 3 * 2048 * per + per // 2 + 1))
+            for nb in (1, per + 1, big):
+                fast = bs % 1024 == 0 or (bs & (bs - 1) == 0 and bs <= 512)  # aligned: rows / sub-KiB kernels
+                mis = int(rng.choice([3, 4] if fast else [0, 3, 4]))
+                t = _region(torch, ctxs[0], bs * nb + 16, SEED ^ (bs * 131 + nb), nb)
+                view = t[mis: mis + bs * nb]
+                want = O.crc32_blocks(view.cpu().numpy(), bs, nthreads=8)
+                for sh, c in enumerate(ctxs):
+                    plan = c.blocks_plan(view.data_ptr(), nb, bs)
+                    # a few unbalanced blocks >= 64 KiB are cut into segments by the fused kernel
+                    assert plan.startswith(f"crc_stride_kernel<G={G},") or (
+                        bs >= 65536 and plan.startswith("crc_ranges_fused_kernel")), plan
+                    got = _u32(c.blocks_dev(view, bs, nblocks=nb))
+                    torch.cuda.synchronize()
+                    assert np.array_equal(got, want), (G, sh, bs, nb, mis, np.nonzero(got != want)[0][:8])
+    finally:
+        for c in ctxs:
+            c.close()
+
+
+@pytest.mark.parametrize("misalign", [0, 1, 2, 3, 4, 8, 13])
+def test_stride_kernel_cost_model_sizes(torch_cuda, ctx, misalign):
+    """Odd sizes through the default plan (cost model), 16 B to 1 MiB - 1, at
+    every kind of base misalignment: bit-exact with the oracle; blocks of 16 B
+    and 4 KiB on unaligned bases (once extents / generic) included."""
+    torch = torch_cuda
+    sizes = [16, 31, 40, 96, 100, 200, 500, 520, 999, 1000, 1500, 2000, 3000, 4096, 4100, 5000, 9999,
+             65535, 100000, (1 << 20) - 1]
+    for bs in sizes:
+        nb = max(3, min(4099, (16 << 20) // bs))
+        t = _region(torch, ctx, bs * nb + 16, SEED ^ (bs + misalign), 7)
+        view = t[misalign: misalign + bs * nb]
+        got = _u32(ctx.blocks_dev(view, bs, nblocks=nb))
+        torch.cuda.synchronize()
+        want = O.crc32_blocks(view.cpu().numpy(), bs, nthreads=8)
+        assert np.array_equal(got, want), (bs, nb, misalign, np.nonzero(got != want)[0][:8])
+
+
+@pytest.mark.slow
+def test_stride_kernel_beyond_4GiB(torch_cuda, ctx):
+    """1.1 M blocks of 4100 B (4.5 GB, group pointers past 2^32) on an
+    odd base: sampled blocks (first, last, every 4096th) against the oracle,
+    and the batch equals the same batch run as two halves."""
+    torch = torch_cuda
+    bs, nb, mis = 4100, 1100000, 5
+    t = _region(torch, ctx, bs * nb + 16, SEED ^ 0x4100, 0)
+    view = t[mis: mis + bs * nb]
+    got = ctx.blocks_dev(view, bs, nblocks=nb)
+    idx = np.unique(np.concatenate([np.arange(0, nb, 4096), [nb - 1]])).astype(np.int64)
+    blocks = view.view(nb, bs).index_select(0, torch.from_numpy(idx).cuda()).cpu().numpy()
+    want = O.crc32_blocks(blocks.reshape(-1), bs, nthreads=8)
+    assert np.array_equal(_u32(got)[idx], want)
+    h = nb // 2 + 1
+    a = ctx.blocks_dev(view, bs, nblocks=h)
+    b = ctx.blocks_dev(view[h * bs:], bs, nblocks=nb - h)
+    torch.cuda.synchronize()
+    assert torch.equal(got, torch.cat([a, b]))
+    del t, view, got, a, b
     torch.cuda.empty_cache()

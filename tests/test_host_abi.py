@@ -222,12 +222,16 @@ def test_path_selection():
     assert C.blocks_path(4096, 10, 3072) == "rows"
     assert C.blocks_path(4096, 10, 256) == "small"
     assert C.blocks_path(4096, 10, 16) == "small"
-    assert C.blocks_path(4096, 10, 100) == "generic"
-    assert C.blocks_path(4097, 10, 100) == "generic"
-    assert C.blocks_path(4097, 10, 4096) == "extents"   # unaligned base
-    assert C.blocks_path(4104, 10, 4096) == "extents"   # 8-byte aligned only
-    assert C.blocks_path(4096, 10, 4100) == "extents"   # not a multiple of 1 KiB
-    assert C.blocks_path(4096, 10, 1000) == "generic"
+    # any other size >= 16 B or base alignment: the uniform-stride kernel
+    assert C.blocks_path(4096, 10, 100) == "stride"
+    assert C.blocks_path(4097, 10, 100) == "stride"
+    assert C.blocks_path(4097, 10, 4096) == "stride"    # unaligned base
+    assert C.blocks_path(4104, 10, 4096) == "stride"    # 8-byte aligned only
+    assert C.blocks_path(4096, 10, 4100) == "stride"    # not a multiple of 1 KiB
+    assert C.blocks_path(4096, 10, 1000) == "stride"
+    assert C.blocks_path(4097, 10, 256) == "stride"     # sub-KiB power of two, unaligned base
+    assert C.blocks_path(4096, 10, 15) == "generic"     # below one 16-B window
+    assert C.blocks_path(4096, 10, 1) == "generic"
 
 
 def test_ctx_create_without_gpu_is_enodev():
