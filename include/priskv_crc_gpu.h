@@ -47,8 +47,9 @@ typedef struct priskv_crc_ctx priskv_crc_ctx;
  * grid from the device's CU count.  *out is set only on success.
  * PRISKV_CRC_SEGMENT=0 in the environment at creation turns off the
  * segmentation of few large blocks / extents, PRISKV_CRC_PRIO=0 the
- * kernels' progress priority and PRISKV_CRC_BALANCE=0 the byte-balanced
- * extents split (measurement only). */
+ * kernels' progress priority, PRISKV_CRC_BALANCE=0 the byte-balanced
+ * extents split and PRISKV_CRC_STRIDE=0 the uniform-stride kernel
+ * (measurement only). */
 int priskv_crc_ctx_create(int device, priskv_crc_ctx **out);
 void priskv_crc_ctx_destroy(priskv_crc_ctx *ctx);
 int priskv_crc_ctx_device(const priskv_crc_ctx *ctx);
@@ -56,10 +57,13 @@ int priskv_crc_ctx_device(const priskv_crc_ctx *ctx);
 /* Device-resident batch: d_base -> nblocks * block_size bytes of device
  * memory; d_out -> uint32_t[nblocks] of device memory.  d_out[i] =
  * priskv_crc32(d_base + i*block_size, block_size).  Asynchronous on `stream`.
- * Any block_size >= 1 and any d_base alignment are accepted; the fast path
- * needs d_base 16-byte aligned and block_size a multiple of 1 KiB (or a power
- * of two in [16, 512]) -- the reference's value blocks (4 KiB-aligned base,
- * power-of-two size, server/memory.c:221,413-417) always qualify. */
+ * Any block_size >= 1 and any d_base alignment are accepted.  A 16-byte
+ * aligned d_base with block_size a multiple of 1 KiB (or a power of two in
+ * [16, 512]) takes the rows (sub-KiB) kernel -- memfile-backed value regions
+ * (4 KiB-aligned base, power-of-two size, server/memory.c:221,413-417) always
+ * do.  Any other block_size >= 16 (the server's -v takes any size up to
+ * 1 MiB, server/server.c:236-244) or base alignment takes the uniform-stride
+ * kernel; full rate needs d_base and block_size multiples of 4. */
 int priskv_crc32_blocks_dev(const priskv_crc_ctx *ctx, const void *d_base, uint64_t nblocks,
                             uint32_t block_size, uint32_t *d_out, void *stream);
 
@@ -175,10 +179,12 @@ int priskv_crc_fill_splitmix_dev(const priskv_crc_ctx *ctx, void *d_dst, uint64_
 /* Which kernel a (d_base, block_size) batch dispatches to: 1 = rows (block
  * a multiple of 1 KiB, 16-byte aligned base: G = 16/32/64 lanes per block;
  * batches of few large blocks are hashed as segments and combined),
- * 2 = extents (any other block >= 1 KiB or any base alignment: one wave per
- * block, masked right-aligned rows + Z_-p tail), 3 = sub-KiB power-of-two blocks,
- * 4 = generic (smaller odd sizes: one thread per block).  For tests and
- * benchmarks; -EINVAL for invalid arguments. */
+ * 3 = sub-KiB power-of-two blocks (16-byte aligned base), 5 = uniform stride
+ * (any other block >= 16 B at any base alignment: rows aligned to each
+ * block's end; few large unbalanced blocks are cut into segments), 4 =
+ * generic (blocks below 16 B: one thread per block).  2 = extents is what a
+ * context created with PRISKV_CRC_STRIDE=0 uses instead of 5 from 1 KiB (and
+ * 4 below).  For tests and benchmarks; -EINVAL for invalid arguments. */
 int priskv_crc32_blocks_path(const void *d_base, uint64_t nblocks, uint32_t block_size);
 
 /* The kernel plan priskv_crc32_blocks_dev would launch for this batch on

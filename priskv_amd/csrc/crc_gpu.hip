@@ -107,7 +107,8 @@ struct priskv_crc_ctx {
                                // extents / generic kernels, as in round 2)
     int stride_g;              // PRISKV_CRC_STRIDE_G: force the stride kernel's G (0 = cost model; tuning)
     int stride_shape;          // PRISKV_CRC_STRIDE_SHAPE: chunk shape variant (tuning)
-    int stride_wgs;            // PRISKV_CRC_STRIDE_WGS: workgroups per CU (tuning)
+    int stride_wgs;            // PRISKV_CRC_STRIDE_WGS=1: one workgroup per CU instead of two (tuning)
+    int stride_runs;           // PRISKV_CRC_STRIDE_RUNS=0: G >= 16 lane groups side by side, not in runs (tuning)
 };
 
 namespace {
@@ -741,34 +742,49 @@ const void *small_fn(int gl, bool prio)
 
 // ---- uniform-stride kernel (odd block sizes, unaligned bases) ------------------
 // G lanes per block with R = ceil(B / 16G) rows; G < 16 only for R = 1 (the
-// set-B row jump exists for G = 16, 32, 64).  Cost model: lane-rows per block
-// plus half a row for the fold, G * (R + 1/2), so the least padding F = R*16G
-// - B and the fewest folds per byte.  4100 B -> G16 x 17 rows, 100 B -> G8 x
-// 1, 1000 B -> G16 x 4.
+// set-B row jump exists for G = 16, 32, 64).  Score = the share of hashed
+// bytes that are block bytes, B / (16G (R + 1/2)) (half a row for the fold),
+// times 0.88 for G <= 16: runs of 256 B or less per block and row read
+// slower from unaligned starts (tools/stride_sweep.py, profiles/r02/stride/:
+// 4100 B G32 5.81 against G16 5.30 TB/s, 1500 B 5.58 / 5.31, 520 B G16
+// 4.42 / G32 3.59).  4100 B -> G32 x 9 rows, 1000 B -> G32 x 2, 520 B ->
+// G16 x 3, 100 B -> G8 x 1.
 struct StridePlan {
     int G;
     uint32_t R;
 };
+constexpr uint32_t kStrideMaxBlock = 64u << 20; // larger odd blocks keep the (segmenting) extents path
 
 StridePlan stride_plan(const priskv_crc_ctx *ctx, uint32_t bs)
 {
     StridePlan best{0, 0};
-    uint64_t bc = ~0ull;
+    double bsc = -1.0;
     for (int pass = 0; pass < 2 && !best.G; pass++)
         for (int G = 2; G <= 64; G *= 2) {
             const uint32_t RB = 16u * (uint32_t)G, R = (uint32_t)(((uint64_t)bs + RB - 1) / RB);
             if ((G < 16 && R > 1) || (pass == 0 && ctx->stride_g && G != ctx->stride_g))
                 continue;
-            const uint64_t cost = (uint64_t)G * (2ull * R + 1);
-            if (cost < bc) {
-                bc = cost;
+            const double score = (double)bs / (RB * (R + 0.5)) * (G <= 16 ? 0.88 : 1.0);
+            if (score > bsc) {
+                bsc = score;
                 best = {G, R};
             }
         }
     return best;
 }
 
-// chunk shapes: 0 = the default, 1-3 tuning variants (PRISKV_CRC_STRIDE_SHAPE)
+// workgroups per CU: two when their LDS fits (64 KiB image + the nibble
+// tables, 16 KiB for G <= 32; G = 64 needs 32 KiB), PRISKV_CRC_STRIDE_WGS=1
+// forces one.  Two gain 5-35 % (sub-KiB most) in profiles/r02/stride/.
+int stride_wgs(const priskv_crc_ctx *ctx, int G) { return G <= 32 ? ctx->stride_wgs : 1; }
+
+// Chunk shapes (rows per chunk CH x chunks in flight NBUF).  0, the
+// default: 8 x 2, two workgroups per CU (+2-8 % over 4 x 2 from 1000 B to
+// 1 MiB, level below; profiles/r02/stride/sweep_tune.jsonl).  1-3: tuning
+// variants (PRISKV_CRC_STRIDE_SHAPE): 4 x 3 (4 x 2 for G < 16), 2 x 4, and
+// 4 x 2 (4 x 3 for G < 16), the first version's.
+constexpr int kStrideShape[4][2] = {{8, 2}, {4, 3}, {2, 4}, {4, 2}};
+
 template <int G>
 const void *stride_fn_g(int shape)
 {
@@ -776,8 +792,8 @@ const void *stride_fn_g(int shape)
     switch (shape) {
     case 1: return reinterpret_cast<const void *>(&crc_stride_kernel<G, 4, small ? 2 : 3, kAux>);
     case 2: return reinterpret_cast<const void *>(&crc_stride_kernel<G, 2, 4, kAux>);
-    case 3: return reinterpret_cast<const void *>(&crc_stride_kernel<G, 8, 2, kAux>);
-    default: return reinterpret_cast<const void *>(&crc_stride_kernel<G, 4, small ? 3 : 2, kAux>);
+    case 3: return reinterpret_cast<const void *>(&crc_stride_kernel<G, 4, small ? 3 : 2, kAux>);
+    default: return reinterpret_cast<const void *>(&crc_stride_kernel<G, 8, 2, kAux>);
     }
 }
 
@@ -799,7 +815,7 @@ const void *stride_fn(int G, int shape)
 bool stride_segmented(const priskv_crc_ctx *ctx, const StridePlan &P, uint64_t nblocks, uint32_t bs)
 {
     const uint64_t NB = 64 / (uint64_t)P.G;
-    const uint64_t waves = (uint64_t)ctx->num_cus * ctx->stride_wgs * kWaves;
+    const uint64_t waves = (uint64_t)ctx->num_cus * stride_wgs(ctx, P.G) * kWaves;
     return ctx->segment && ctx->fused && bs >= kSegMinLen && nblocks <= kFusedMaxExtents &&
            !balanced((nblocks + NB - 1) / NB, waves);
 }
@@ -811,26 +827,26 @@ int launch_stride(const priskv_crc_ctx *ctx, const uint8_t *base, uint64_t nbloc
     if (stride_segmented(ctx, P, nblocks, bs))
         return launch_fused(ctx, base, nblocks, nullptr, nullptr, bs, bs, out, s);
     const uint64_t NB = 64 / (uint64_t)P.G;
-    const uint64_t max_wgs = (uint64_t)ctx->num_cus * ctx->stride_wgs;
-    const uint64_t ngroups = (nblocks + NB - 1) / NB;
-    // the kernel counts a wave's rows in 32 bits: cap groups per launch
-    const uint64_t cap = max_wgs * kWaves * ((1ull << 31) / P.R - 1);
+    const uint64_t max_wgs = (uint64_t)ctx->num_cus * stride_wgs(ctx, P.G);
+    // a wave's range is one buffer descriptor with 31-bit offsets, and its
+    // NB lane groups may run up to NB - 1 blocks past it: cap blocks per launch
+    const uint64_t per_wave = ((1ull << 31) - 1) / bs - NB; // >= 1: bs <= kStrideMaxBlock
+    const uint64_t cap = max_wgs * kWaves * per_wave;
     const uint32_t *img = ctx->d_lds_image[P.G == 64 ? 0 : (P.G == 32 ? 1 : 2)]; // set B unused for G < 16 (R = 1)
     const uint32_t *nib = ctx->d_nibrep[log2u((uint32_t)P.G)];
     const void *fn = stride_fn(P.G, ctx->stride_shape);
-    uint32_t R = P.R;
-    for (uint64_t done = 0; done < ngroups;) {
-        const uint64_t n = ngroups - done < cap ? ngroups - done : cap;
-        const uint64_t want = (n + kWaves - 1) / kWaves;
+    uint32_t R = P.R, runs = (uint32_t)ctx->stride_runs;
+    for (uint64_t done = 0; done < nblocks;) {
+        uint64_t nb = nblocks - done < cap ? nblocks - done : cap;
+        const uint64_t want = (nb + NB * kWaves - 1) / (NB * kWaves); // about NB blocks per wave and up
         const uint32_t grid = (uint32_t)(want < max_wgs ? want : max_wgs);
-        const uint8_t *b = base + done * NB * bs;
-        uint64_t nb = nblocks - done * NB;
-        nb = nb < n * NB ? nb : n * NB;
-        uint32_t *o = out + done * NB;
-        void *args[] = {(void *)&b, (void *)&nb, (void *)&bs, (void *)&R, (void *)&img, (void *)&nib, (void *)&o};
+        const uint8_t *b = base + done * bs;
+        uint32_t *o = out + done;
+        void *args[] = {(void *)&b,   (void *)&nb, (void *)&bs, (void *)&R,
+                        (void *)&img, (void *)&nib, (void *)&o, (void *)&runs};
         if (int rc = herr(hipLaunchKernel(fn, dim3(grid), dim3(kThreads), args, 0, s)))
             return rc;
-        done += n;
+        done += nb;
     }
     return 0;
 }
@@ -841,8 +857,10 @@ int launch_blocks(const priskv_crc_ctx *ctx, const uint8_t *base, uint64_t nbloc
     const int path = choose_path(base, bs, ctx->stride);
     if (path == PATH_ROWS)
         return launch_rows(ctx, base, nblocks, bs, out, s);
-    if (path == PATH_STRIDE)
+    if (path == PATH_STRIDE && bs <= kStrideMaxBlock)
         return launch_stride(ctx, base, nblocks, bs, out, s);
+    if (path == PATH_STRIDE) // blocks beyond 64 MiB: extents, cut into segments
+        return launch_extents(ctx, base, nblocks, nullptr, nullptr, bs, bs, out, s);
     if (path == PATH_SMALL) {
         const int gl = log2u(bs / 16); // G = 1 << gl
         const uint64_t per = 1024 / bs; // blocks per row
@@ -963,13 +981,15 @@ int priskv_crc32_blocks_plan(const priskv_crc_ctx *ctx, const void *d_base, uint
     const char *fused_name = "crc_ranges_fused_kernel (few large values: segments, one launch)";
     if (path == PATH_STRIDE) {
         const StridePlan P = stride_plan(ctx, block_size);
-        if (stride_segmented(ctx, P, nblocks, block_size)) {
+        if (block_size > kStrideMaxBlock) {
+            w = snprintf(buf, len, "%s", extents_segmented(ctx, nblocks, block_size) && ctx->fused ? fused_name
+                                                                                                   : "crc_ranges_kernel (extents)");
+        } else if (stride_segmented(ctx, P, nblocks, block_size)) {
             w = snprintf(buf, len, "%s", fused_name);
         } else {
-            static const int kShapeCh[4][2] = {{4, 0}, {4, 1}, {2, 4}, {8, 2}}; // CH, NBUF (0/1: 3/2 or 2/3 by G)
             const int sh = ctx->stride_shape;
-            const int ch = kShapeCh[sh][0];
-            const int nbuf = sh == 0 ? (P.G < 16 ? 3 : 2) : (sh == 1 ? (P.G < 16 ? 2 : 3) : kShapeCh[sh][1]);
+            const int ch = kStrideShape[sh][0];
+            const int nbuf = sh == 1 ? (P.G < 16 ? 2 : 3) : (sh == 3 ? (P.G < 16 ? 3 : 2) : kStrideShape[sh][1]);
             w = snprintf(buf, len, "crc_stride_kernel<G=%d,CH=%d,NBUF=%d,nt> (%u rows of %u B per block, %u B in front)",
                          P.G, ch, nbuf, P.R, 16u * P.G, P.R * 16u * P.G - block_size);
         }
@@ -1057,9 +1077,11 @@ int priskv_crc_ctx_create(int device, priskv_crc_ctx **out)
         c->stride_shape = 0;
         if (const char *m = getenv("PRISKV_CRC_STRIDE_SHAPE"))
             c->stride_shape = atoi(m) & 3;
-        c->stride_wgs = 1;
+        const char *re = getenv("PRISKV_CRC_STRIDE_RUNS");
+        c->stride_runs = !(re && !strcmp(re, "0"));
+        c->stride_wgs = 2;
         if (const char *m = getenv("PRISKV_CRC_STRIDE_WGS"))
-            c->stride_wgs = atoi(m) == 2 ? 2 : 1;
+            c->stride_wgs = atoi(m) == 1 ? 1 : 2;
         c->seg_max_extents = kSegMaxExtents;
         c->tile_min_bytes = kTileMinBytes;
         c->tile_bytes = kTileBytes;

@@ -1002,10 +1002,11 @@ def test_blocks_plan_strings(torch_cuda, ctx):
     assert "crc_combine_segments_kernel" in ctx.blocks_plan(base, 1000, 1 << 20)
     assert ctx.blocks_plan(base, 100, 256) == "crc_small_kernel<G=16>"
     # odd sizes and unaligned bases: the uniform-stride kernel
-    assert ctx.blocks_plan(base + 1, 100, 4096).startswith("crc_stride_kernel<G=16,CH=4,NBUF=2,nt> (16 rows of 256 B")
-    assert ctx.blocks_plan(base, 100, 4100).startswith("crc_stride_kernel<G=16,CH=4,NBUF=2,nt> (17 rows of 256 B "
-                                                       "per block, 252 B in front)")
-    assert ctx.blocks_plan(base, 100, 100).startswith("crc_stride_kernel<G=8,CH=4,NBUF=3,nt> (1 rows of 128 B")
+    assert ctx.blocks_plan(base + 1, 100, 4096).startswith("crc_stride_kernel<G=32,CH=8,NBUF=2,nt> (8 rows of 512 B")
+    assert ctx.blocks_plan(base, 100, 4100).startswith("crc_stride_kernel<G=32,CH=8,NBUF=2,nt> (9 rows of 512 B "
+                                                       "per block, 508 B in front)")
+    assert ctx.blocks_plan(base, 100, 520).startswith("crc_stride_kernel<G=16,CH=8,NBUF=2,nt> (3 rows of 256 B")
+    assert ctx.blocks_plan(base, 100, 100).startswith("crc_stride_kernel<G=8,CH=8,NBUF=2,nt> (1 rows of 128 B")
     assert ctx.blocks_plan(base, 100, 15) == "crc_generic_kernel"
     off = _ctx_env(PRISKV_CRC_STRIDE="0")  # round 2's dispatch
     assert off.blocks_plan(base + 1, 100, 4096) == "crc_ranges_kernel (extents)"
