@@ -1309,3 +1309,29 @@ def test_stride_kernel_beyond_4GiB(torch_cuda, ctx):
     assert torch.equal(got, torch.cat([a, b]))
     del t, view, got, a, b
     torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("bs,nb,mis,kind,noseg", [((64 << 20) - 3, 3, 1, "crc_ranges_fused_kernel", False),
+                                                ((64 << 20) - 3, 3, 1, "crc_stride_kernel<G=32,", True),
+                                                ((64 << 20) + 5, 2, 0, "crc_ranges_fused_kernel", False),
+                                                ((5 << 20) + 7, 400, 2, "crc_stride_kernel<G=32,", True),
+                                                (4100, 2049, 4, "crc_stride_kernel<G=32,", False)])
+def test_stride_kernel_large_and_limit_blocks(torch_cuda, ctx, ctx_noseg, bs, nb, mis, kind, noseg):
+    """Odd block sizes at both sides of the stride kernel's 64 MiB limit (a
+    few such blocks are cut into segments by the fused kernel, or with
+    segmentation off hashed whole by the stride kernel: 2 x 10 241 rows per
+    block; more than 64 MiB always keeps the extents path), a 2 GB batch of
+    5 MiB + 7 B blocks, and a batch whose last lane-group runs are short:
+    the oracle's CRCs."""
+    torch = torch_cuda
+    ctx = ctx_noseg if noseg else ctx
+    t = _region(torch, ctx, bs * nb + 16, SEED ^ (bs + nb), 5)
+    view = t[mis: mis + bs * nb]
+    plan = ctx.blocks_plan(view.data_ptr(), nb, bs)
+    assert plan.startswith(kind), plan
+    got = _u32(ctx.blocks_dev(view, bs, nblocks=nb))
+    torch.cuda.synchronize()
+    want = O.crc32_blocks(view.cpu().numpy(), bs, nthreads=16)
+    assert np.array_equal(got, want), (bs, nb, np.nonzero(got != want)[0][:8])
+    del t, view
+    torch.cuda.empty_cache()
