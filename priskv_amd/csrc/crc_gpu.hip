@@ -108,6 +108,7 @@ struct priskv_crc_ctx {
     int stride_g;              // PRISKV_CRC_STRIDE_G: force the stride kernel's G (0 = cost model; tuning)
     int stride_shape;          // PRISKV_CRC_STRIDE_SHAPE: chunk shape variant (tuning)
     int stride_wgs;            // PRISKV_CRC_STRIDE_WGS=1: one workgroup per CU instead of two (tuning)
+    int stride_funnel;         // PRISKV_CRC_STRIDE_FUNNEL=0: odd sizes / bases load unaligned (tuning)
     int stride_runs;           // PRISKV_CRC_STRIDE_RUNS=0: G >= 16 lane groups side by side, not in runs (tuning)
 };
 
@@ -785,10 +786,15 @@ int stride_wgs(const priskv_crc_ctx *ctx, int G) { return G <= 32 ? ctx->stride_
 // 4 x 2 (4 x 3 for G < 16), the first version's.
 constexpr int kStrideShape[4][2] = {{8, 2}, {4, 3}, {2, 4}, {4, 2}};
 
+// odd: a block size or base that is not a multiple of 4 -- the default
+// shape has a variant with aligned loads and funnel shifts; the
+// tuning shapes load at the unaligned rate
 template <int G>
-const void *stride_fn_g(int shape)
+const void *stride_fn_g(int shape, bool odd)
 {
     constexpr bool small = G < 16;
+    if (odd && shape == 0)
+        return reinterpret_cast<const void *>(&crc_stride_kernel<G, 8, 2, kAux, true>);
     switch (shape) {
     case 1: return reinterpret_cast<const void *>(&crc_stride_kernel<G, 4, small ? 2 : 3, kAux>);
     case 2: return reinterpret_cast<const void *>(&crc_stride_kernel<G, 2, 4, kAux>);
@@ -797,15 +803,15 @@ const void *stride_fn_g(int shape)
     }
 }
 
-const void *stride_fn(int G, int shape)
+const void *stride_fn(int G, int shape, bool odd)
 {
     switch (G) {
-    case 2: return stride_fn_g<2>(shape);
-    case 4: return stride_fn_g<4>(shape);
-    case 8: return stride_fn_g<8>(shape);
-    case 16: return stride_fn_g<16>(shape);
-    case 32: return stride_fn_g<32>(shape);
-    default: return stride_fn_g<64>(shape);
+    case 2: return stride_fn_g<2>(shape, odd);
+    case 4: return stride_fn_g<4>(shape, odd);
+    case 8: return stride_fn_g<8>(shape, odd);
+    case 16: return stride_fn_g<16>(shape, odd);
+    case 32: return stride_fn_g<32>(shape, odd);
+    default: return stride_fn_g<64>(shape, odd);
     }
 }
 
@@ -834,13 +840,13 @@ int launch_stride(const priskv_crc_ctx *ctx, const uint8_t *base, uint64_t nbloc
     const uint64_t cap = max_wgs * kWaves * per_wave;
     const uint32_t *img = ctx->d_lds_image[P.G == 64 ? 0 : (P.G == 32 ? 1 : 2)]; // set B unused for G < 16 (R = 1)
     const uint32_t *nib = ctx->d_nibrep[log2u((uint32_t)P.G)];
-    const void *fn = stride_fn(P.G, ctx->stride_shape);
     uint32_t R = P.R, runs = (uint32_t)ctx->stride_runs;
     for (uint64_t done = 0; done < nblocks;) {
         uint64_t nb = nblocks - done < cap ? nblocks - done : cap;
         const uint64_t want = (nb + NB * kWaves - 1) / (NB * kWaves); // about NB blocks per wave and up
         const uint32_t grid = (uint32_t)(want < max_wgs ? want : max_wgs);
         const uint8_t *b = base + done * bs;
+        const void *fn = stride_fn(P.G, ctx->stride_shape, ctx->stride_funnel && (((uintptr_t)b | bs) & 3u));
         uint32_t *o = out + done;
         void *args[] = {(void *)&b,   (void *)&nb, (void *)&bs, (void *)&R,
                         (void *)&img, (void *)&nib, (void *)&o, (void *)&runs};
@@ -1077,6 +1083,8 @@ int priskv_crc_ctx_create(int device, priskv_crc_ctx **out)
         c->stride_shape = 0;
         if (const char *m = getenv("PRISKV_CRC_STRIDE_SHAPE"))
             c->stride_shape = atoi(m) & 3;
+        const char *fu = getenv("PRISKV_CRC_STRIDE_FUNNEL");
+        c->stride_funnel = !(fu && !strcmp(fu, "0"));
         const char *re = getenv("PRISKV_CRC_STRIDE_RUNS");
         c->stride_runs = !(re && !strcmp(re, "0"));
         c->stride_wgs = 2;

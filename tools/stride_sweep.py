@@ -4,7 +4,7 @@ against round 2's dispatch (PRISKV_CRC_STRIDE=0: extents kernel from 1 KiB,
 generic kernel below) and against its own tuning variants (chunk shape,
 forced G, two workgroups per CU), all contexts in one process, interleaved.
 
-    python tools/stride_sweep.py [GiB per call=1] [rounds=2] [variants=all|tune|g|base]
+    python tools/stride_sweep.py [GiB per call=1] [rounds=2] [variants=all|tune|g|runs|funnel|base]
 
 One JSON line per (round, size, context): HIP-event time per call over
 `steps` back-to-back calls, TB/s of algorithmic bytes (block + 4 B CRC), and
@@ -53,6 +53,8 @@ def main():
         for sh in (1, 2, 3):
             ctxs[f"shape{sh}"] = ctx_env(PRISKV_CRC_STRIDE_SHAPE=sh)
         ctxs["w1"] = ctx_env(PRISKV_CRC_STRIDE_WGS=1)
+    elif which == "funnel":
+        ctxs["nofunnel"] = ctx_env(PRISKV_CRC_STRIDE_FUNNEL=0)
     elif which == "runs":
         ctxs["noruns"] = ctx_env(PRISKV_CRC_STRIDE_RUNS=0)
         ctxs["noruns_sh3"] = ctx_env(PRISKV_CRC_STRIDE_RUNS=0, PRISKV_CRC_STRIDE_SHAPE=3)
