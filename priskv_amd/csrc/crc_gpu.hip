@@ -755,6 +755,18 @@ struct StridePlan {
     uint32_t R;
 };
 constexpr uint32_t kStrideMaxBlock = 64u << 20; // larger odd blocks keep the (segmenting) extents path
+// Odd block sizes or bases (not multiples of 4) from 32 KiB up: the extents
+// kernel's 16-B aligned windows and one fold per block beat the funnel
+// shifts by 5-10 % (8 KiB 5.16 / 4.65, 16 KiB 5.29 / 5.09, 32 KiB 5.14 /
+// 5.45, 64 KiB 5.28 / 5.56, 256 KiB 5.16 / 5.71 TB/s stride / extents,
+// profiles/r02/stride/sweep_oddlarge.jsonl)
+constexpr uint32_t kStrideOddMax = 32u << 10;
+
+bool stride_to_extents(const priskv_crc_ctx *ctx, const void *base, uint32_t bs)
+{
+    const bool odd = (((uintptr_t)base | bs) & 3u) != 0;
+    return bs > kStrideMaxBlock || (odd && bs >= kStrideOddMax && ctx->stride_funnel);
+}
 
 StridePlan stride_plan(const priskv_crc_ctx *ctx, uint32_t bs)
 {
@@ -863,9 +875,9 @@ int launch_blocks(const priskv_crc_ctx *ctx, const uint8_t *base, uint64_t nbloc
     const int path = choose_path(base, bs, ctx->stride);
     if (path == PATH_ROWS)
         return launch_rows(ctx, base, nblocks, bs, out, s);
-    if (path == PATH_STRIDE && bs <= kStrideMaxBlock)
+    if (path == PATH_STRIDE && !stride_to_extents(ctx, base, bs))
         return launch_stride(ctx, base, nblocks, bs, out, s);
-    if (path == PATH_STRIDE) // blocks beyond 64 MiB: extents, cut into segments
+    if (path == PATH_STRIDE) // odd blocks from 32 KiB, blocks beyond 64 MiB: extents (segmented when few)
         return launch_extents(ctx, base, nblocks, nullptr, nullptr, bs, bs, out, s);
     if (path == PATH_SMALL) {
         const int gl = log2u(bs / 16); // G = 1 << gl
@@ -987,7 +999,7 @@ int priskv_crc32_blocks_plan(const priskv_crc_ctx *ctx, const void *d_base, uint
     const char *fused_name = "crc_ranges_fused_kernel (few large values: segments, one launch)";
     if (path == PATH_STRIDE) {
         const StridePlan P = stride_plan(ctx, block_size);
-        if (block_size > kStrideMaxBlock) {
+        if (stride_to_extents(ctx, d_base, block_size)) {
             w = snprintf(buf, len, "%s", extents_segmented(ctx, nblocks, block_size) && ctx->fused ? fused_name
                                                                                                    : "crc_ranges_kernel (extents)");
         } else if (stride_segmented(ctx, P, nblocks, block_size)) {

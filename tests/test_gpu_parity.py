@@ -1259,9 +1259,12 @@ def test_stride_kernel_every_g_and_shape(torch_cuda, G):
                 want = O.crc32_blocks(view.cpu().numpy(), bs, nthreads=8)
                 for sh, c in enumerate(ctxs):
                     plan = c.blocks_plan(view.data_ptr(), nb, bs)
-                    # a few unbalanced blocks >= 64 KiB are cut into segments by the fused kernel
+                    # a few unbalanced blocks >= 64 KiB are cut into segments by the fused
+                    # kernel; odd sizes / bases from 32 KiB take the extents kernel
+                    odd_big = bs >= 32768 and ((bs | mis) & 3) != 0
                     assert plan.startswith(f"crc_stride_kernel<G={G},") or (
-                        bs >= 65536 and plan.startswith("crc_ranges_fused_kernel")), plan
+                        bs >= 65536 and plan.startswith("crc_ranges_fused_kernel")) or (
+                        odd_big and plan.startswith("crc_ranges_kernel")), plan
                     got = _u32(c.blocks_dev(view, bs, nblocks=nb))
                     torch.cuda.synchronize()
                     assert np.array_equal(got, want), (G, sh, bs, nb, mis, np.nonzero(got != want)[0][:8])
@@ -1312,17 +1315,20 @@ def test_stride_kernel_beyond_4GiB(torch_cuda, ctx):
 
 
 @pytest.mark.parametrize("bs,nb,mis,kind,noseg", [((64 << 20) - 3, 3, 1, "crc_ranges_fused_kernel", False),
-                                                ((64 << 20) - 3, 3, 1, "crc_stride_kernel<G=32,", True),
+                                                ((64 << 20) - 4, 3, 4, "crc_stride_kernel<G=32,", True),
                                                 ((64 << 20) + 5, 2, 0, "crc_ranges_fused_kernel", False),
-                                                ((5 << 20) + 7, 400, 2, "crc_stride_kernel<G=32,", True),
+                                                ((5 << 20) + 8, 400, 4, "crc_stride_kernel<G=32,", True),
+                                                ((5 << 20) + 7, 400, 2, "crc_ranges_kernel (extents)", True),
+                                                (32767, 3000, 1, "crc_stride_kernel<G=32,", False),
+                                                (32769, 3000, 0, "crc_ranges_kernel (extents)", False),
                                                 (4100, 2049, 4, "crc_stride_kernel<G=32,", False)])
 def test_stride_kernel_large_and_limit_blocks(torch_cuda, ctx, ctx_noseg, bs, nb, mis, kind, noseg):
-    """Odd block sizes at both sides of the stride kernel's 64 MiB limit (a
-    few such blocks are cut into segments by the fused kernel, or with
-    segmentation off hashed whole by the stride kernel: 2 x 10 241 rows per
-    block; more than 64 MiB always keeps the extents path), a 2 GB batch of
-    5 MiB + 7 B blocks, and a batch whose last lane-group runs are short:
-    the oracle's CRCs."""
+    """Blocks at both sides of the stride kernel's limits: 64 MiB (a few such
+    blocks are cut into segments by the fused kernel, or with segmentation
+    off hashed whole by the stride kernel: 2 x 131 072 rows; more than
+    64 MiB keeps the extents path) and 32 KiB for odd sizes (the extents
+    kernel from there), 2 GB batches of 5 MiB + 8 / + 7 B blocks, and a
+    batch whose last lane-group runs are short: the oracle's CRCs."""
     torch = torch_cuda
     ctx = ctx_noseg if noseg else ctx
     t = _region(torch, ctx, bs * nb + 16, SEED ^ (bs + nb), 5)

@@ -4,7 +4,7 @@ against round 2's dispatch (PRISKV_CRC_STRIDE=0: extents kernel from 1 KiB,
 generic kernel below) and against its own tuning variants (chunk shape,
 forced G, two workgroups per CU), all contexts in one process, interleaved.
 
-    python tools/stride_sweep.py [GiB per call=1] [rounds=2] [variants=all|tune|g|runs|funnel|base]
+    python tools/stride_sweep.py [GiB per call=1] [rounds=2] [variants=all|tune|g|runs|funnel|oddlarge|base]
 
 One JSON line per (round, size, context): HIP-event time per call over
 `steps` back-to-back calls, TB/s of algorithmic bytes (block + 4 B CRC), and
@@ -71,7 +71,10 @@ def main():
     total = int(gib * (1 << 30))
     stream = torch.cuda.Stream()
     for rnd in range(rounds):
-        for bs, mis in CASES:
+        cases = CASES
+        if which == "oddlarge":  # odd sizes of 8 KiB-256 KiB: stride (funnel) against the extents kernel
+            cases = [(8193, 0), (16385, 0), (32769, 0), (65537, 0), (131073, 0), (262145, 0), (16384, 1), (65536, 3)]
+        for bs, mis in cases:
             nb = total // bs
             t = torch.empty(nb * bs + 64, dtype=torch.uint8, device="cuda")
             ctxs["stride"].fill_splitmix(t, SEED ^ bs, 0)
