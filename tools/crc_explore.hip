@@ -749,6 +749,10 @@ int main(int argc, char **argv)
     all.push_back(ROOF_VARIANT_W(32, 8, 2, 2, 1, 41, 39));
     all.push_back(ROOF_VARIANT(64, 4, 2, 2, 2));
     all.push_back(ROOF_VARIANT_W(64, 4, 2, 2, 2, 41, 39));
+    // the round-2 4 KiB plan's own access pattern (G64 CH4 NBUF3, one
+    // workgroup per CU, 31:29), with and without the weights
+    all.push_back(ROOF_VARIANT_W(64, 4, 3, 2, 1, 31, 29));
+    all.push_back(ROOF_VARIANT_W(64, 4, 3, 2, 1, 0, 0));
     // EXPLORE_FILTER="a,b,c": keep only variants whose name contains one of the substrings
     std::vector<std::string> filt;
     if (const char *f = getenv("EXPLORE_FILTER")) {
