@@ -753,6 +753,13 @@ int main(int argc, char **argv)
     // workgroup per CU, 31:29), with and without the weights
     all.push_back(ROOF_VARIANT_W(64, 4, 3, 2, 1, 31, 29));
     all.push_back(ROOF_VARIANT_W(64, 4, 3, 2, 1, 0, 0));
+    // more bytes in flight: deeper pipelines, more waves per CU
+    all.push_back(ROOF_VARIANT_W(64, 4, 4, 2, 1, 31, 29));
+    all.push_back(ROOF_VARIANT_W(64, 4, 6, 2, 1, 31, 29));
+    all.push_back(ROOF_VARIANT_W(64, 4, 2, 2, 2, 31, 29));
+    all.push_back(ROOF_VARIANT_W(64, 4, 3, 2, 2, 31, 29));
+    all.push_back(ROOF_VARIANT_W(64, 4, 2, 2, 3, 31, 29));
+    all.push_back(ROOF_VARIANT_W(64, 2, 4, 2, 1, 31, 29));
     // EXPLORE_FILTER="a,b,c": keep only variants whose name contains one of the substrings
     std::vector<std::string> filt;
     if (const char *f = getenv("EXPLORE_FILTER")) {
