@@ -109,7 +109,7 @@ struct priskv_crc_ctx {
     int stride_shape;          // PRISKV_CRC_STRIDE_SHAPE: chunk shape variant (tuning)
     int stride_wgs;            // PRISKV_CRC_STRIDE_WGS=1: one workgroup per CU instead of two (tuning)
     int stride_funnel;         // PRISKV_CRC_STRIDE_FUNNEL=0: odd sizes / bases load unaligned (tuning)
-    int stride_runs;           // PRISKV_CRC_STRIDE_RUNS=0: G >= 16 lane groups side by side, not in runs (tuning)
+    int stride_runs;           // PRISKV_CRC_STRIDE_RUNS=1: G >= 16 lane groups in runs, not side by side (tuning)
 };
 
 namespace {
@@ -777,7 +777,11 @@ StridePlan stride_plan(const priskv_crc_ctx *ctx, uint32_t bs)
             const uint32_t RB = 16u * (uint32_t)G, R = (uint32_t)(((uint64_t)bs + RB - 1) / RB);
             if ((G < 16 && R > 1) || (pass == 0 && ctx->stride_g && G != ctx->stride_g))
                 continue;
-            const double score = (double)bs / (RB * (R + 0.5)) * (G <= 16 ? 0.88 : 1.0);
+            // rows used / rows loaded (half a row of front slack on average),
+            // G <= 16 marked down; from 16 rows of 1 KiB, G = 64 wins outright
+            // (+1-9 % over G = 32 from 16 KiB to 100 KB, -2 % at 12 KiB;
+            // profiles/r02/stride/sweep_large.jsonl)
+            const double score = (G == 64 && R >= 16) ? 2.0 : (double)bs / (RB * (R + 0.5)) * (G <= 16 ? 0.88 : 1.0);
             if (score > bsc) {
                 bsc = score;
                 best = {G, R};
@@ -788,12 +792,13 @@ StridePlan stride_plan(const priskv_crc_ctx *ctx, uint32_t bs)
 
 // workgroups per CU: two when their LDS fits (64 KiB image + the nibble
 // tables, 16 KiB for G <= 32; G = 64 needs 32 KiB), PRISKV_CRC_STRIDE_WGS=1
-// forces one.  Two gain 5-35 % (sub-KiB most) in profiles/r02/stride/.
+// forces one.  Two gain 18-28 % below 1 KiB, 0-12 % from 1000 to 4097 B
+// (profiles/r02/stride/sweep_retune.jsonl, order-rotated).
 int stride_wgs(const priskv_crc_ctx *ctx, int G) { return G <= 32 ? ctx->stride_wgs : 1; }
 
 // Chunk shapes (rows per chunk CH x chunks in flight NBUF).  0, the
-// default: 8 x 2, two workgroups per CU (+2-8 % over 4 x 2 from 1000 B to
-// 1 MiB, level below; profiles/r02/stride/sweep_tune.jsonl).  1-3: tuning
+// default: 8 x 2, two workgroups per CU (the shapes differed by 2-8 % either
+// way with the context order; profiles/r02/stride/sweep_tune.jsonl).  1-3: tuning
 // variants (PRISKV_CRC_STRIDE_SHAPE): 4 x 3 (4 x 2 for G < 16), 2 x 4, and
 // 4 x 2 (4 x 3 for G < 16), the first version's.
 constexpr int kStrideShape[4][2] = {{8, 2}, {4, 3}, {2, 4}, {4, 2}};
@@ -1098,7 +1103,7 @@ int priskv_crc_ctx_create(int device, priskv_crc_ctx **out)
         const char *fu = getenv("PRISKV_CRC_STRIDE_FUNNEL");
         c->stride_funnel = !(fu && !strcmp(fu, "0"));
         const char *re = getenv("PRISKV_CRC_STRIDE_RUNS");
-        c->stride_runs = !(re && !strcmp(re, "0"));
+        c->stride_runs = re && !strcmp(re, "1");
         c->stride_wgs = 2;
         if (const char *m = getenv("PRISKV_CRC_STRIDE_WGS"))
             c->stride_wgs = atoi(m) == 1 ? 1 : 2;

@@ -1007,8 +1007,11 @@ def test_blocks_plan_strings(torch_cuda, ctx):
                                                        "per block, 508 B in front)")
     assert ctx.blocks_plan(base, 100, 520).startswith("crc_stride_kernel<G=16,CH=8,NBUF=2,nt> (3 rows of 256 B")
     assert ctx.blocks_plan(base, 100, 100).startswith("crc_stride_kernel<G=8,CH=8,NBUF=2,nt> (1 rows of 128 B")
+    assert ctx.blocks_plan(base, 100, 12292).startswith("crc_stride_kernel<G=32,CH=8,NBUF=2,nt> (25 rows of 512 B")
+    # from 16 rows of 1 KiB: G = 64
+    assert ctx.blocks_plan(base, 100, 16388).startswith("crc_stride_kernel<G=64,CH=8,NBUF=2,nt> (17 rows of 1024 B")
     assert ctx.blocks_plan(base, 100, 15) == "crc_generic_kernel"
-    off = _ctx_env(PRISKV_CRC_STRIDE="0")  # round 2's dispatch
+    off =_ctx_env(PRISKV_CRC_STRIDE="0")  # round 2's dispatch
     assert off.blocks_plan(base + 1, 100, 4096) == "crc_ranges_kernel (extents)"
     assert off.blocks_plan(base, 100, 100) == "crc_generic_kernel"
     off.close()
@@ -1246,6 +1249,8 @@ def test_stride_kernel_every_g_and_shape(torch_cuda, G):
     per wave with a ragged end."""
     torch = torch_cuda
     ctxs = [_ctx_env(PRISKV_CRC_STRIDE_G=G, PRISKV_CRC_STRIDE_SHAPE=sh) for sh in range(4)]
+    ctxs.append(_ctx_env(PRISKV_CRC_STRIDE_G=G, PRISKV_CRC_STRIDE_RUNS=1))  # G >= 16: groups in runs
+    ctxs.append(_ctx_env(PRISKV_CRC_STRIDE_G=G, PRISKV_CRC_STRIDE_FUNNEL=0))  # odd sizes: unaligned loads
     per = 64 // G
     rng = np.random.default_rng(G)
     try:
@@ -1265,7 +1270,9 @@ def test_stride_kernel_every_g_and_shape(torch_cuda, G):
                     assert plan.startswith(f"crc_stride_kernel<G={G},") or (
                         bs >= 65536 and plan.startswith("crc_ranges_fused_kernel")) or (
                         odd_big and plan.startswith("crc_ranges_kernel")), plan
-                    got = _u32(c.blocks_dev(view, bs, nblocks=nb))
+                    # a sentinel-filled output: a CRC the kernel fails to store shows
+                    out = torch.full((nb,), 0x5A5A5A5A, dtype=torch.int32, device="cuda")
+                    got = _u32(c.blocks_dev(view, bs, out=out, nblocks=nb))
                     torch.cuda.synchronize()
                     assert np.array_equal(got, want), (G, sh, bs, nb, mis, np.nonzero(got != want)[0][:8])
     finally:
@@ -1285,7 +1292,8 @@ def test_stride_kernel_cost_model_sizes(torch_cuda, ctx, misalign):
         nb = max(3, min(4099, (16 << 20) // bs))
         t = _region(torch, ctx, bs * nb + 16, SEED ^ (bs + misalign), 7)
         view = t[misalign: misalign + bs * nb]
-        got = _u32(ctx.blocks_dev(view, bs, nblocks=nb))
+        out = torch.full((nb,), 0x5A5A5A5A, dtype=torch.int32, device="cuda")  # unwritten CRCs show
+        got = _u32(ctx.blocks_dev(view, bs, out=out, nblocks=nb))
         torch.cuda.synchronize()
         want = O.crc32_blocks(view.cpu().numpy(), bs, nthreads=8)
         assert np.array_equal(got, want), (bs, nb, misalign, np.nonzero(got != want)[0][:8])
