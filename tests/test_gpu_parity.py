@@ -1323,17 +1323,17 @@ def test_stride_kernel_beyond_4GiB(torch_cuda, ctx):
 
 
 @pytest.mark.parametrize("bs,nb,mis,kind,noseg", [((64 << 20) - 3, 3, 1, "crc_ranges_fused_kernel", False),
-                                                ((64 << 20) - 4, 3, 4, "crc_stride_kernel<G=32,", True),
+                                                ((64 << 20) - 4, 3, 4, "crc_stride_kernel<G=64,", True),
                                                 ((64 << 20) + 5, 2, 0, "crc_ranges_fused_kernel", False),
-                                                ((5 << 20) + 8, 400, 4, "crc_stride_kernel<G=32,", True),
+                                                ((5 << 20) + 8, 400, 4, "crc_stride_kernel<G=64,", True),
                                                 ((5 << 20) + 7, 400, 2, "crc_ranges_kernel (extents)", True),
-                                                (32767, 3000, 1, "crc_stride_kernel<G=32,", False),
+                                                (32767, 3000, 1, "crc_stride_kernel<G=64,", False),
                                                 (32769, 3000, 0, "crc_ranges_kernel (extents)", False),
                                                 (4100, 2049, 4, "crc_stride_kernel<G=32,", False)])
 def test_stride_kernel_large_and_limit_blocks(torch_cuda, ctx, ctx_noseg, bs, nb, mis, kind, noseg):
     """Blocks at both sides of the stride kernel's limits: 64 MiB (a few such
     blocks are cut into segments by the fused kernel, or with segmentation
-    off hashed whole by the stride kernel: 2 x 131 072 rows; more than
+    off hashed whole by the stride kernel: 65 536 rows of 1 KiB; more than
     64 MiB keeps the extents path) and 32 KiB for odd sizes (the extents
     kernel from there), 2 GB batches of 5 MiB + 8 / + 7 B blocks, and a
     batch whose last lane-group runs are short: the oracle's CRCs."""
