@@ -110,6 +110,8 @@ struct priskv_crc_ctx {
     int stride_wgs;            // PRISKV_CRC_STRIDE_WGS=1: one workgroup per CU instead of two (tuning)
     int stride_funnel;         // PRISKV_CRC_STRIDE_FUNNEL=0: odd sizes / bases load unaligned (tuning)
     int stride_runs;           // PRISKV_CRC_STRIDE_RUNS=1: G >= 16 lane groups in runs, not side by side (tuning)
+    uint64_t stride_max;       // blocks from this size (multiples of 4) take the extents path,
+    uint64_t stride_odd_max;   // and odd ones from this (PRISKV_CRC_STRIDE_MAX_KIB sets both; tuning, tests)
 };
 
 namespace {
@@ -755,17 +757,26 @@ struct StridePlan {
     uint32_t R;
 };
 constexpr uint32_t kStrideMaxBlock = 64u << 20; // larger odd blocks keep the (segmenting) extents path
-// Odd block sizes or bases (not multiples of 4) from 32 KiB up: the extents
+// Odd block sizes or bases (not multiples of 4) from 8 KiB up: the extents
 // kernel's 16-B aligned windows and one fold per block beat the funnel
-// shifts by 5-10 % (8 KiB 5.16 / 4.65, 16 KiB 5.29 / 5.09, 32 KiB 5.14 /
-// 5.45, 64 KiB 5.28 / 5.56, 256 KiB 5.16 / 5.71 TB/s stride / extents,
-// profiles/r02/stride/sweep_oddlarge.jsonl)
-constexpr uint32_t kStrideOddMax = 32u << 10;
+// shifts (8193 B 5.86 / 5.64, 16 385 B 6.32 / 5.19, 16 KiB on base + 1
+// 6.46 / 5.43, level from 32 KiB + 1 TB/s extents / stride; order-rotated,
+// profiles/r02/stride/sweep_oddlarge_r2.jsonl; 4097 B 4.80 / 5.52,
+// sweep_final_r2.jsonl)
+constexpr uint32_t kStrideOddMax = 8u << 10;
+// Block sizes and bases that are multiples of 4, from 16 KiB up: the extents
+// kernel leads by 1-7 % (16 388 B 6.30 / 5.89, 32 772 B 6.62 / 6.18,
+// 100 000 B 6.33 / 6.21, 64 KiB on base + 4 6.43 / 6.37 TB/s extents /
+// stride; at 8196 B the stride kernel leads, 5.92 / 5.83;
+// profiles/r02/stride/sweep_cross.jsonl).  PRISKV_CRC_STRIDE_MAX_KIB moves
+// the limit (tuning, and the tests of the kernel's large-block limits).
+constexpr uint32_t kStrideMax = 16u << 10;
 
 bool stride_to_extents(const priskv_crc_ctx *ctx, const void *base, uint32_t bs)
 {
     const bool odd = (((uintptr_t)base | bs) & 3u) != 0;
-    return bs > kStrideMaxBlock || (odd && bs >= kStrideOddMax && ctx->stride_funnel);
+    return bs > kStrideMaxBlock || (odd && bs >= ctx->stride_odd_max && ctx->stride_funnel) ||
+           (!odd && bs >= ctx->stride_max);
 }
 
 StridePlan stride_plan(const priskv_crc_ctx *ctx, uint32_t bs)
@@ -882,7 +893,7 @@ int launch_blocks(const priskv_crc_ctx *ctx, const uint8_t *base, uint64_t nbloc
         return launch_rows(ctx, base, nblocks, bs, out, s);
     if (path == PATH_STRIDE && !stride_to_extents(ctx, base, bs))
         return launch_stride(ctx, base, nblocks, bs, out, s);
-    if (path == PATH_STRIDE) // odd blocks from 32 KiB, blocks beyond 64 MiB: extents (segmented when few)
+    if (path == PATH_STRIDE) // odd blocks from 8 KiB, others from 16 KiB, beyond 64 MiB: extents (segmented when few)
         return launch_extents(ctx, base, nblocks, nullptr, nullptr, bs, bs, out, s);
     if (path == PATH_SMALL) {
         const int gl = log2u(bs / 16); // G = 1 << gl
@@ -1104,6 +1115,10 @@ int priskv_crc_ctx_create(int device, priskv_crc_ctx **out)
         c->stride_funnel = !(fu && !strcmp(fu, "0"));
         const char *re = getenv("PRISKV_CRC_STRIDE_RUNS");
         c->stride_runs = re && !strcmp(re, "1");
+        c->stride_max = kStrideMax;
+        c->stride_odd_max = kStrideOddMax;
+        if (const char *m = getenv("PRISKV_CRC_STRIDE_MAX_KIB"))
+            c->stride_max = c->stride_odd_max = strtoull(m, nullptr, 10) << 10;
         c->stride_wgs = 2;
         if (const char *m = getenv("PRISKV_CRC_STRIDE_WGS"))
             c->stride_wgs = atoi(m) == 1 ? 1 : 2;

@@ -1008,8 +1008,11 @@ def test_blocks_plan_strings(torch_cuda, ctx):
     assert ctx.blocks_plan(base, 100, 520).startswith("crc_stride_kernel<G=16,CH=8,NBUF=2,nt> (3 rows of 256 B")
     assert ctx.blocks_plan(base, 100, 100).startswith("crc_stride_kernel<G=8,CH=8,NBUF=2,nt> (1 rows of 128 B")
     assert ctx.blocks_plan(base, 100, 12292).startswith("crc_stride_kernel<G=32,CH=8,NBUF=2,nt> (25 rows of 512 B")
-    # from 16 rows of 1 KiB: G = 64
-    assert ctx.blocks_plan(base, 100, 16388).startswith("crc_stride_kernel<G=64,CH=8,NBUF=2,nt> (17 rows of 1024 B")
+    # the extents kernel from 8 KiB for odd sizes, from 16 KiB for multiples of 4
+    assert ctx.blocks_plan(base, 100, 8191).startswith("crc_stride_kernel<G=32,CH=8,NBUF=2,nt> (16 rows of 512 B")
+    assert ctx.blocks_plan(base, 100, 8193) == "crc_ranges_kernel (extents)"
+    assert ctx.blocks_plan(base, 100, 16380).startswith("crc_stride_kernel<G=64,CH=8,NBUF=2,nt> (16 rows of 1024 B")
+    assert ctx.blocks_plan(base, 100, 16388) == "crc_ranges_kernel (extents)"
     assert ctx.blocks_plan(base, 100, 15) == "crc_generic_kernel"
     off =_ctx_env(PRISKV_CRC_STRIDE="0")  # round 2's dispatch
     assert off.blocks_plan(base + 1, 100, 4096) == "crc_ranges_kernel (extents)"
@@ -1251,6 +1254,7 @@ def test_stride_kernel_every_g_and_shape(torch_cuda, G):
     ctxs = [_ctx_env(PRISKV_CRC_STRIDE_G=G, PRISKV_CRC_STRIDE_SHAPE=sh) for sh in range(4)]
     ctxs.append(_ctx_env(PRISKV_CRC_STRIDE_G=G, PRISKV_CRC_STRIDE_RUNS=1))  # G >= 16: groups in runs
     ctxs.append(_ctx_env(PRISKV_CRC_STRIDE_G=G, PRISKV_CRC_STRIDE_FUNNEL=0))  # odd sizes: unaligned loads
+    ctxs.append(_ctx_env(PRISKV_CRC_STRIDE_G=G, PRISKV_CRC_STRIDE_MAX_KIB=131072))  # large blocks stay here
     per = 64 // G
     rng = np.random.default_rng(G)
     try:
@@ -1265,8 +1269,9 @@ def test_stride_kernel_every_g_and_shape(torch_cuda, G):
                 for sh, c in enumerate(ctxs):
                     plan = c.blocks_plan(view.data_ptr(), nb, bs)
                     # a few unbalanced blocks >= 64 KiB are cut into segments by the fused
-                    # kernel; odd sizes / bases from 32 KiB take the extents kernel
-                    odd_big = bs >= 32768 and ((bs | mis) & 3) != 0
+                    # kernel; odd sizes / bases from 8 KiB take the extents kernel
+                    odd = ((bs | mis) & 3) != 0
+                    odd_big = bs >= (8192 if odd else 16384) and c is not ctxs[-1]
                     assert plan.startswith(f"crc_stride_kernel<G={G},") or (
                         bs >= 65536 and plan.startswith("crc_ranges_fused_kernel")) or (
                         odd_big and plan.startswith("crc_ranges_kernel")), plan
@@ -1322,23 +1327,31 @@ def test_stride_kernel_beyond_4GiB(torch_cuda, ctx):
     torch.cuda.empty_cache()
 
 
-@pytest.mark.parametrize("bs,nb,mis,kind,noseg", [((64 << 20) - 3, 3, 1, "crc_ranges_fused_kernel", False),
-                                                ((64 << 20) - 4, 3, 4, "crc_stride_kernel<G=64,", True),
-                                                ((64 << 20) + 5, 2, 0, "crc_ranges_fused_kernel", False),
-                                                ((5 << 20) + 8, 400, 4, "crc_stride_kernel<G=64,", True),
-                                                ((5 << 20) + 7, 400, 2, "crc_ranges_kernel (extents)", True),
-                                                (32767, 3000, 1, "crc_stride_kernel<G=64,", False),
-                                                (32769, 3000, 0, "crc_ranges_kernel (extents)", False),
-                                                (4100, 2049, 4, "crc_stride_kernel<G=32,", False)])
-def test_stride_kernel_large_and_limit_blocks(torch_cuda, ctx, ctx_noseg, bs, nb, mis, kind, noseg):
+# noseg: segmentation off; wide: PRISKV_CRC_STRIDE_MAX_KIB = 128 MiB, so
+# blocks that are multiples of 4 from 16 KiB stay on the stride kernel
+@pytest.mark.parametrize("bs,nb,mis,kind,noseg,wide", [((64 << 20) - 3, 3, 1, "crc_ranges_fused_kernel", False, False),
+                                                     ((64 << 20) - 4, 3, 4, "crc_stride_kernel<G=64,", True, True),
+                                                     ((64 << 20) - 4, 3, 4, "crc_ranges_kernel (extents)", True, False),
+                                                     ((64 << 20) + 5, 2, 0, "crc_ranges_fused_kernel", False, False),
+                                                     ((5 << 20) + 8, 400, 4, "crc_stride_kernel<G=64,", True, True),
+                                                     ((5 << 20) + 7, 400, 2, "crc_ranges_kernel (extents)", True,
+                                                      False),
+                                                     (8191, 6000, 1, "crc_stride_kernel<G=32,", False, False),
+                                                     (8193, 6000, 0, "crc_ranges_kernel (extents)", False, False),
+                                                     (16388, 3000, 0, "crc_ranges_kernel (extents)", False, False),
+                                                     (4100, 2049, 4, "crc_stride_kernel<G=32,", False, False)])
+def test_stride_kernel_large_and_limit_blocks(torch_cuda, ctx, ctx_noseg, bs, nb, mis, kind, noseg, wide):
     """Blocks at both sides of the stride kernel's limits: 64 MiB (a few such
     blocks are cut into segments by the fused kernel, or with segmentation
-    off hashed whole by the stride kernel: 65 536 rows of 1 KiB; more than
-    64 MiB keeps the extents path) and 32 KiB for odd sizes (the extents
-    kernel from there), 2 GB batches of 5 MiB + 8 / + 7 B blocks, and a
-    batch whose last lane-group runs are short: the oracle's CRCs."""
+    off and the size limit raised hashed whole by the stride kernel: 65 536
+    rows of 1 KiB; more than 64 MiB keeps the extents path), 8 KiB for odd
+    sizes and 16 KiB for multiples of 4 (the extents kernel from there), 2 GB
+    batches of 5 MiB + 8 / + 7 B blocks, and a batch whose last lane-group
+    runs are short: the oracle's CRCs."""
     torch = torch_cuda
     ctx = ctx_noseg if noseg else ctx
+    if wide:
+        ctx = _ctx_env(PRISKV_CRC_SEGMENT="0", PRISKV_CRC_STRIDE_MAX_KIB=131072)
     t = _region(torch, ctx, bs * nb + 16, SEED ^ (bs + nb), 5)
     view = t[mis: mis + bs * nb]
     plan = ctx.blocks_plan(view.data_ptr(), nb, bs)
@@ -1347,5 +1360,7 @@ def test_stride_kernel_large_and_limit_blocks(torch_cuda, ctx, ctx_noseg, bs, nb
     torch.cuda.synchronize()
     want = O.crc32_blocks(view.cpu().numpy(), bs, nthreads=16)
     assert np.array_equal(got, want), (bs, nb, np.nonzero(got != want)[0][:8])
+    if wide:
+        ctx.close()
     del t, view
     torch.cuda.empty_cache()

@@ -84,6 +84,9 @@ def main():
     stream = torch.cuda.Stream()
     for rnd in range(rounds):
         cases = CASES
+        if which == "cross":  # stride (default) against round 2's extents kernel on multi-row blocks
+            cases = [(8196, 0), (16388, 0), (24580, 0), (32772, 0), (49156, 0), (65540, 0), (100000, 0),
+                     (16384, 4), (65536, 4), (262148, 0)]
         if which == "large":
             cases = [(4100, 0), (8196, 0), (12292, 0), (16388, 0), (32772, 0), (65540, 0), (100000, 0),
                      (300004, 0), (1000004, 0), (65536, 4)]
