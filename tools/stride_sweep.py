@@ -61,6 +61,8 @@ def main():
         ctxs["w1_runs"] = ctx_env(PRISKV_CRC_STRIDE_WGS=1, PRISKV_CRC_STRIDE_RUNS=1)
         ctxs["w1_sh1"] = ctx_env(PRISKV_CRC_STRIDE_WGS=1, PRISKV_CRC_STRIDE_SHAPE=1)
         ctxs["g64"] = ctx_env(PRISKV_CRC_STRIDE_G=64)
+    elif which == "runsab":  # lane groups side by side (default) against runs, at bench.py's batch size
+        ctxs = {"default": ctxs["stride"], "runs": ctx_env(PRISKV_CRC_STRIDE_RUNS=1)}
     elif which == "large":  # G for multi-row blocks (the cost model's G = 64 threshold)
         ctxs = {"default": ctxs["stride"]}
         for g in (16, 32, 64):
@@ -84,6 +86,8 @@ def main():
     stream = torch.cuda.Stream()
     for rnd in range(rounds):
         cases = CASES
+        if which == "runsab":
+            cases = [(4100, 0), (4097, 0), (3000, 0), (1000, 0), (520, 0)]
         if which == "cross":  # stride (default) against round 2's extents kernel on multi-row blocks
             cases = [(8196, 0), (16388, 0), (24580, 0), (32772, 0), (49156, 0), (65540, 0), (100000, 0),
                      (16384, 4), (65536, 4), (262148, 0)]
