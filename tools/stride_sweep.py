@@ -86,6 +86,8 @@ def main():
     stream = torch.cuda.Stream()
     for rnd in range(rounds):
         cases = CASES
+        if which == "refine":  # the stride / extents size limits, between the measured points
+            cases = [(5121, 0), (6145, 0), (7169, 0), (8193, 0), (10244, 0), (12292, 0), (14340, 0), (16388, 0)]
         if which == "runsab":
             cases = [(4100, 0), (4097, 0), (3000, 0), (1000, 0), (520, 0)]
         if which == "cross":  # stride (default) against round 2's extents kernel on multi-row blocks
