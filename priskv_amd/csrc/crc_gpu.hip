@@ -757,20 +757,19 @@ struct StridePlan {
     uint32_t R;
 };
 constexpr uint32_t kStrideMaxBlock = 64u << 20; // larger odd blocks keep the (segmenting) extents path
-// Odd block sizes or bases (not multiples of 4) from 8 KiB up: the extents
-// kernel's 16-B aligned windows and one fold per block beat the funnel
-// shifts (8193 B 5.86 / 5.64, 16 385 B 6.32 / 5.19, 16 KiB on base + 1
-// 6.46 / 5.43, level from 32 KiB + 1 TB/s extents / stride; order-rotated,
-// profiles/r02/stride/sweep_oddlarge_r2.jsonl; 4097 B 4.80 / 5.52,
-// sweep_final_r2.jsonl)
-constexpr uint32_t kStrideOddMax = 8u << 10;
-// Block sizes and bases that are multiples of 4, from 16 KiB up: the extents
-// kernel leads by 1-7 % (16 388 B 6.30 / 5.89, 32 772 B 6.62 / 6.18,
-// 100 000 B 6.33 / 6.21, 64 KiB on base + 4 6.43 / 6.37 TB/s extents /
-// stride; at 8196 B the stride kernel leads, 5.92 / 5.83;
-// profiles/r02/stride/sweep_cross.jsonl).  PRISKV_CRC_STRIDE_MAX_KIB moves
-// the limit (tuning, and the tests of the kernel's large-block limits).
-constexpr uint32_t kStrideMax = 16u << 10;
+// Odd block sizes or bases (not multiples of 4) from 4.5 KiB, other sizes
+// from 9 KiB: the extents kernel's 16-B aligned windows and one fold per
+// block beat the stride kernel's per-row work once a block spans 9-10 of its
+// rows.  TB/s extents / stride, order-rotated, one process: odd 4097 B 4.80
+// / 5.52 (sweep_final_r2.jsonl), 5121 B 5.64 / 5.47, 7169 B 6.06 / 5.55,
+// 16 385 B 6.32 / 5.19 (sweep_refine, sweep_oddlarge_r2); multiples of 4
+// 8196 B 5.83 / 5.92 (sweep_cross), 10 244 B 6.22 / 6.01, 14 340 B 6.42 /
+// 5.99, 32 772 B 6.62 / 6.18 (profiles/r02/stride/).  The limits sit midway
+// between the last size the stride kernel led and the first it did not.
+// PRISKV_CRC_STRIDE_MAX_KIB sets both (tuning, and the tests of the
+// kernel's large-block limits).
+constexpr uint32_t kStrideOddMax = 4608;
+constexpr uint32_t kStrideMax = 9u << 10;
 
 bool stride_to_extents(const priskv_crc_ctx *ctx, const void *base, uint32_t bs)
 {
@@ -893,7 +892,7 @@ int launch_blocks(const priskv_crc_ctx *ctx, const uint8_t *base, uint64_t nbloc
         return launch_rows(ctx, base, nblocks, bs, out, s);
     if (path == PATH_STRIDE && !stride_to_extents(ctx, base, bs))
         return launch_stride(ctx, base, nblocks, bs, out, s);
-    if (path == PATH_STRIDE) // odd blocks from 8 KiB, others from 16 KiB, beyond 64 MiB: extents (segmented when few)
+    if (path == PATH_STRIDE) // odd blocks from 4.5 KiB, others from 9 KiB, beyond 64 MiB: extents (segmented when few)
         return launch_extents(ctx, base, nblocks, nullptr, nullptr, bs, bs, out, s);
     if (path == PATH_SMALL) {
         const int gl = log2u(bs / 16); // G = 1 << gl

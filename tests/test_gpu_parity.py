@@ -1007,12 +1007,11 @@ def test_blocks_plan_strings(torch_cuda, ctx):
                                                        "per block, 508 B in front)")
     assert ctx.blocks_plan(base, 100, 520).startswith("crc_stride_kernel<G=16,CH=8,NBUF=2,nt> (3 rows of 256 B")
     assert ctx.blocks_plan(base, 100, 100).startswith("crc_stride_kernel<G=8,CH=8,NBUF=2,nt> (1 rows of 128 B")
-    assert ctx.blocks_plan(base, 100, 12292).startswith("crc_stride_kernel<G=32,CH=8,NBUF=2,nt> (25 rows of 512 B")
-    # the extents kernel from 8 KiB for odd sizes, from 16 KiB for multiples of 4
-    assert ctx.blocks_plan(base, 100, 8191).startswith("crc_stride_kernel<G=32,CH=8,NBUF=2,nt> (16 rows of 512 B")
-    assert ctx.blocks_plan(base, 100, 8193) == "crc_ranges_kernel (extents)"
-    assert ctx.blocks_plan(base, 100, 16380).startswith("crc_stride_kernel<G=64,CH=8,NBUF=2,nt> (16 rows of 1024 B")
-    assert ctx.blocks_plan(base, 100, 16388) == "crc_ranges_kernel (extents)"
+    # the extents kernel from 4.5 KiB for odd sizes, from 9 KiB for multiples of 4
+    assert ctx.blocks_plan(base, 100, 4607).startswith("crc_stride_kernel<G=32,CH=8,NBUF=2,nt> (9 rows of 512 B")
+    assert ctx.blocks_plan(base, 100, 4609) == "crc_ranges_kernel (extents)"
+    assert ctx.blocks_plan(base, 100, 9212).startswith("crc_stride_kernel<G=32,CH=8,NBUF=2,nt> (18 rows of 512 B")
+    assert ctx.blocks_plan(base, 100, 9220) == "crc_ranges_kernel (extents)"
     assert ctx.blocks_plan(base, 100, 15) == "crc_generic_kernel"
     off =_ctx_env(PRISKV_CRC_STRIDE="0")  # round 2's dispatch
     assert off.blocks_plan(base + 1, 100, 4096) == "crc_ranges_kernel (extents)"
@@ -1269,9 +1268,9 @@ def test_stride_kernel_every_g_and_shape(torch_cuda, G):
                 for sh, c in enumerate(ctxs):
                     plan = c.blocks_plan(view.data_ptr(), nb, bs)
                     # a few unbalanced blocks >= 64 KiB are cut into segments by the fused
-                    # kernel; odd sizes / bases from 8 KiB take the extents kernel
+                    # kernel; odd sizes / bases from 4.5 KiB (others from 9 KiB) take the extents kernel
                     odd = ((bs | mis) & 3) != 0
-                    odd_big = bs >= (8192 if odd else 16384) and c is not ctxs[-1]
+                    odd_big = bs >= (4608 if odd else 9216) and c is not ctxs[-1]
                     assert plan.startswith(f"crc_stride_kernel<G={G},") or (
                         bs >= 65536 and plan.startswith("crc_ranges_fused_kernel")) or (
                         odd_big and plan.startswith("crc_ranges_kernel")), plan
@@ -1336,16 +1335,16 @@ def test_stride_kernel_beyond_4GiB(torch_cuda, ctx):
                                                      ((5 << 20) + 8, 400, 4, "crc_stride_kernel<G=64,", True, True),
                                                      ((5 << 20) + 7, 400, 2, "crc_ranges_kernel (extents)", True,
                                                       False),
-                                                     (8191, 6000, 1, "crc_stride_kernel<G=32,", False, False),
-                                                     (8193, 6000, 0, "crc_ranges_kernel (extents)", False, False),
+                                                     (4607, 6000, 1, "crc_stride_kernel<G=32,", False, False),
+                                                     (4609, 6000, 0, "crc_ranges_kernel (extents)", False, False),
                                                      (16388, 3000, 0, "crc_ranges_kernel (extents)", False, False),
                                                      (4100, 2049, 4, "crc_stride_kernel<G=32,", False, False)])
 def test_stride_kernel_large_and_limit_blocks(torch_cuda, ctx, ctx_noseg, bs, nb, mis, kind, noseg, wide):
     """Blocks at both sides of the stride kernel's limits: 64 MiB (a few such
     blocks are cut into segments by the fused kernel, or with segmentation
     off and the size limit raised hashed whole by the stride kernel: 65 536
-    rows of 1 KiB; more than 64 MiB keeps the extents path), 8 KiB for odd
-    sizes and 16 KiB for multiples of 4 (the extents kernel from there), 2 GB
+    rows of 1 KiB; more than 64 MiB keeps the extents path), 4.5 KiB for odd
+    sizes and 9 KiB for multiples of 4 (the extents kernel from there), 2 GB
     batches of 5 MiB + 8 / + 7 B blocks, and a batch whose last lane-group
     runs are short: the oracle's CRCs."""
     torch = torch_cuda
