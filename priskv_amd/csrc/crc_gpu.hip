@@ -790,7 +790,8 @@ StridePlan stride_plan(const priskv_crc_ctx *ctx, uint32_t bs)
             // rows used / rows loaded (half a row of front slack on average),
             // G <= 16 marked down; from 16 rows of 1 KiB, G = 64 wins outright
             // (+1-9 % over G = 32 from 16 KiB to 100 KB, -2 % at 12 KiB;
-            // profiles/r02/stride/sweep_large.jsonl)
+            // profiles/r02/stride/sweep_large.jsonl) -- such blocks take the
+            // extents kernel unless PRISKV_CRC_STRIDE_MAX_KIB raises the limit
             const double score = (G == 64 && R >= 16) ? 2.0 : (double)bs / (RB * (R + 0.5)) * (G <= 16 ? 0.88 : 1.0);
             if (score > bsc) {
                 bsc = score;
