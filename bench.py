@@ -12,33 +12,48 @@ its own 4 GiB shard -- the next 1 Mi blocks of one global region -- and
 checksums it with no data-path collective ("weak" scaling); the barrier and
 the max-over-ranks reduction are the benchmark contract, not part of the path.
 
-Extra keys of the ONE JSON line rank 0 prints:
-  tib           BASELINE.json configs[3] measured in the same run at every N:
-                each rank's shard of the 16 Mi x 64 KiB (1 TiB at 8 GPUs)
-                region, 2 Mi x 64 KiB = 128 GiB per GPU, filled on the device;
-                aggregate GiB/s over the N ranks (barrier + max over ranks),
-                with sampled blocks (first, last, every 4096th of every
-                shard) checked bit-exactly against the CPU oracle
+Extra keys of the ONE JSON line rank 0 prints (every BASELINE config that
+fits a GPU is measured in the same run, each timed outside the headline's
+timed region, with barrier + max over ranks at N > 1):
+  sweep         configs[2]: 64 Ki x 64 KiB and 4 Ki x 1 MiB (4 GiB per GPU
+                each), device-resident, each with its kernel's roofline and
+                every block checked bit-exactly against the CPU oracle
+  tib           configs[3]: each rank's 2 Mi x 64 KiB = 128 GiB shard of the
+                16 Mi x 64 KiB (1 TiB at 8 GPUs) region; sampled parity
+                (first, last, every 4096th block of every shard)
+  streamed      configs[4]: the headline's 1 Mi x 4 KiB blocks from HOST
+                memory, end to end (H2D copies, kernels and D2H of the CRCs
+                overlapped on 3 streams, priskv_crc32_blocks_host): pinned
+                (registered) and pageable, roofline against PCIe Gen5 x16
   roofline      dominant kernel (crc_rows_kernel) vs the HBM roof: algorithmic
                 bytes per launch / average launch time (HIP events on the launch
                 stream); traffic = PMC-measured HBM bytes per launch for this
                 workload when profiles/ holds a matching measurement, else null
-  cold_ms       the first full pass after the device has idled (clock ramp
-                included), beside the steady-state `value`
-  pipelined     the same K passes round-robin on 2 streams (reported beside,
-                never instead of, `value`)
+  cold          the first full pass over a fresh region after the device has
+                idled (clock ramp included), and the same after idle over an
+                already-hashed region, beside the steady-state `value`
+  ranks, dist   per-rank device identity (PCI address, UUID) and kernel time,
+                process-group backend and world size: a line at N > 1 shows
+                that N distinct GPUs did the work
   cpu_baseline  rank 0, every N, after all GPU work: the reference's own
                 server/crc.c (compiled unmodified into oracle/_ref at -O2, its
                 release flag, and -O0, the shipped default) timed on a bounded
                 sample of the same blocks, 1 thread and every thread this
                 process may use; the CRCs double as a bit-exact spot check
-  parity        result of comparing the GPU CRCs with those CPU samples
+  parity        every headline block of every rank against the CPU oracle
+
+Multi-rank launches must map ranks to distinct GPUs: a rank whose LOCAL_RANK
+has no device of its own, or two ranks on one device, exit with status 3
+before any measurement.  PRISKV_BENCH_REHEARSAL=1 lifts that for a
+rehearsal of the N > 1 path on a one-GPU box (ranks share the device over
+gloo), and the line then says so.
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
 import sys
 import time
 
@@ -49,27 +64,29 @@ sys.path.insert(0, ROOT)
 
 METRIC = "GiB/s CRC over device-resident value blocks at 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
+PCIE_PEAK_GBS = 63.0   # host link, PCIe Gen5 x16 (MI355X_MICROARCH.md chip table)
 SEED = 0x5EED5EED
 RAMP_MIN_S = 1.0
 RAMP_MAX_S = 4.0
 COLD_IDLE_S = 1.0
+EXIT_DEVICES = 3
 
 CONFIGS = {
     # name: (block_size, nblocks per GPU, description)
     "default": (4096, 1 << 20, "1Mi x 4KiB value blocks per GPU, device-resident (4 GiB/GPU; BASELINE configs[1])"),
-    "sweep64k": (65536, 1 << 16, "64Ki x 64KiB value blocks per GPU, device-resident (4 GiB/GPU)"),
-    "sweep1m": (1 << 20, 1 << 12, "4Ki x 1MiB value blocks per GPU, device-resident (4 GiB/GPU)"),
+    "sweep64k": (65536, 1 << 16, "64Ki x 64KiB value blocks per GPU, device-resident (4 GiB/GPU; BASELINE configs[2])"),
+    "sweep1m": (1 << 20, 1 << 12, "4Ki x 1MiB value blocks per GPU, device-resident (4 GiB/GPU; BASELINE configs[2])"),
     "tib": (65536, 1 << 21, "2Mi x 64KiB value blocks per GPU (128 GiB/GPU; 1 TiB at 8 GPUs; BASELINE configs[3])"),
 }
-TIB_BS, TIB_NB = CONFIGS["tib"][0], CONFIGS["tib"][1]
+SWEEP = (("64KiB", "sweep64k"), ("1MiB", "sweep1m"))
 
 
-def parse():
+def parse(argv=None):
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=50)
     p.add_argument("--warmup", type=int, default=10)
-    p.add_argument("--config", default="default", choices=sorted(CONFIGS) + ["streamed"])
+    p.add_argument("--config", default="default", choices=sorted(CONFIGS))
     p.add_argument("--block-size", type=int, default=None)
     p.add_argument("--nblocks", type=int, default=None)
     p.add_argument("--cpu-sample-bytes", type=int, default=2 << 30,
@@ -77,11 +94,57 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-tib", action="store_true", help="skip the configs[3] (128 GiB/GPU) leg")
     p.add_argument("--tib-steps", type=int, default=10)
-    p.add_argument("--pipeline-streams", type=int, default=2,
-                   help="streams for the reported-beside pipelined pass (0 = skip it)")
-    return p.parse_args()
+    p.add_argument("--no-sweep", action="store_true", help="skip the configs[2] (64 KiB / 1 MiB) legs")
+    p.add_argument("--sweep-steps", type=int, default=20)
+    p.add_argument("--no-streamed", action="store_true", help="skip the configs[4] (host-resident) leg")
+    p.add_argument("--streamed-steps", type=int, default=5)
+    return p.parse_args(argv)
 
 
+# ---------------------------------------------------------------- rank <-> device
+def device_guard(world: int, local: int, ndev: int, rehearsal: bool):
+    """None if this rank may run, else the reason it must not.  One process
+    per GPU: LOCAL_RANK must name a device of its own.  A rehearsal (several
+    ranks on a one-GPU box, gloo) is allowed only when asked for."""
+    if ndev < 1:
+        return "no GPU visible to this process"
+    if local < 0:
+        return f"bad LOCAL_RANK {local}"
+    if local >= ndev and not rehearsal:
+        return (f"LOCAL_RANK {local} of WORLD_SIZE {world} has no GPU of its own ({ndev} visible): "
+                f"ranks would share a device; set PRISKV_BENCH_REHEARSAL=1 only for a one-box rehearsal")
+    return None
+
+
+def duplicate_devices(infos):
+    """Groups of ranks that report the same physical device (host + PCI
+    address, or UUID when the PCI address is unknown)."""
+    seen = {}
+    for i in infos:
+        key = (i["host"], i["pci"] or i["uuid"] or f"dev{i['device']}")
+        seen.setdefault(key, []).append(i["rank"])
+    return [r for r in seen.values() if len(r) > 1]
+
+
+def device_info(torch, rank, local, gpu):
+    p = torch.cuda.get_device_properties(gpu)
+    dom, bus, dv = (getattr(p, k, None) for k in ("pci_domain_id", "pci_bus_id", "pci_device_id"))
+    pci = f"{dom:04x}:{bus:02x}:{dv:02x}" if None not in (dom, bus, dv) else None
+    uuid = str(getattr(p, "uuid", "") or "") or None
+    return {"rank": rank, "local_rank": local, "host": socket.gethostname(), "device": gpu, "pci": pci,
+            "uuid": uuid, "name": p.name}
+
+
+def gather_obj(obj, world):
+    import torch.distributed as dist
+    if world == 1:
+        return [obj]
+    out = [None] * world
+    dist.all_gather_object(out, obj)
+    return out
+
+
+# ---------------------------------------------------------------- helpers
 def load_traffic(block_size: int, nblocks: int):
     """HBM bytes per launch from a committed rocprofv3 PMC summary, if one matches."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
@@ -108,10 +171,10 @@ def cpu_threads():
 def ramp(fn, stream, torch, window=16, min_s=RAMP_MIN_S, max_s=RAMP_MAX_S):
     """Untimed launches until the device is in its steady state.  A fresh
     process runs 5-8 % slow for about its first second of GPU work, and the
-    first ~10 launches after idle up to 40 % (profiles/r01/clock_ramp.txt,
-    profiles/r02/bench_bisect_*.json): launch back-to-back windows of
-    `window` steps and stop once two consecutive windows agree within 0.5 %
-    (after at least min_s, at most max_s).  Returns (launches, seconds)."""
+    first ~10 launches after idle up to 40 %: launch
+    back-to-back windows of `window` steps and stop once two consecutive
+    windows agree within 0.5 % (after at least min_s, at most max_s).
+    Returns (launches, seconds)."""
     n = 0
     prev = None
     t0 = time.perf_counter()
@@ -119,7 +182,7 @@ def ramp(fn, stream, torch, window=16, min_s=RAMP_MIN_S, max_s=RAMP_MAX_S):
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record(stream)
         for _ in range(window):
-            fn(n)
+            fn()
             n += 1
         e1.record(stream)
         e1.synchronize()
@@ -130,263 +193,183 @@ def ramp(fn, stream, torch, window=16, min_s=RAMP_MIN_S, max_s=RAMP_MAX_S):
         prev = cur
 
 
-def main():
-    args = parse()
-    import torch
-    import torch.distributed as dist
+class Bench:
+    """Per-rank state shared by the legs."""
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus and rank == 0:
-        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
-    # one process per GPU; modulo only matters for a multi-rank rehearsal on a
-    # one-GPU box (PRISKV_BENCH_BACKEND=gloo), never on the 8-GPU node
-    gpu = local % max(1, torch.cuda.device_count())
-    torch.cuda.set_device(gpu)
-    dev = torch.device("cuda", gpu)
-    backend = os.environ.get("PRISKV_BENCH_BACKEND", "nccl")  # nccl == RCCL on ROCm
-    if world > 1:
-        if backend == "nccl":
-            dist.init_process_group("nccl", device_id=dev)
-        else:
-            dist.init_process_group(backend)
+    def __init__(self, args, torch, dist, world, rank, dev, ctx):
+        self.args, self.torch, self.dist = args, torch, dist
+        self.world, self.rank, self.dev, self.ctx = world, rank, dev, ctx
 
-    from priskv_amd import CrcContext, as_u32
+    def barrier(self):
+        if self.world > 1:
+            self.dist.barrier()
 
-    if args.config == "streamed":
-        return streamed(args, torch, rank, world)
+    def max(self, v):
+        from priskv_amd.shard import max_over_ranks
+        return max_over_ranks(v, device=self.dev)
 
-    bs, nb, desc = CONFIGS[args.config]
-    if args.block_size:
-        bs = args.block_size
-    if args.nblocks:
-        nb = args.nblocks
-    from priskv_amd.shard import max_over_ranks, shard_blocks, shard_word_offset
-    ctx = CrcContext(gpu)
-    # weak scaling: the global region has world * nb blocks; this rank's shard
-    # is its contiguous range of them (no data-path collective)
-    first, nb = shard_blocks(world * nb, rank, world)
-    region = torch.empty(bs * nb, dtype=torch.uint8, device=dev)
-    ctx.fill_splitmix(region, SEED, word_offset=shard_word_offset(first, bs))
-    out = torch.empty(nb, dtype=torch.int32, device=dev)
-    # a created stream: torch's null stream costs ~1 % per launch
-    # (profiles/r02/bench_bisect_*.json); the device-wide synchronize()
-    # around the timed region covers every stream
-    stream = torch.cuda.Stream(device=dev)
-    sync = torch.cuda.synchronize
+    def all_ok(self, ok: bool) -> bool:
+        return self.max(0.0 if ok else 1.0) == 0.0
 
-    def barrier():
-        if world > 1:
-            dist.barrier()
-
-    def step(_i=0):
-        ctx.blocks_dev(region, bs, out=out, stream=stream)
-
-    for _ in range(args.warmup):
-        step()
-    sync()
-    nramp, ramp_s = ramp(step, stream, torch)
-
-    trace = os.environ.get("PRISKV_BENCH_TRACE")
-    if trace:  # per-step kernel times of a separate, untimed pass (diagnostics only)
-        evs = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
-        evs[0].record(stream)
-        for i in range(args.steps):
+    def timed(self, step, stream, k):
+        """k back-to-back steps between barrier + synchronize on both sides:
+        (max-over-ranks wall seconds, this rank's kernel ms per step)."""
+        torch = self.torch
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        self.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        ev0.record(stream)
+        for _ in range(k):
             step()
-            evs[i + 1].record(stream)
-        sync()
-        print("per-step ms:", " ".join(f"{evs[i].elapsed_time(evs[i + 1]):.3f}" for i in range(args.steps)),
-              file=sys.stderr)
+        ev1.record(stream)
+        torch.cuda.synchronize()
+        self.barrier()
+        el = time.perf_counter() - t0
+        return self.max(el), ev0.elapsed_time(ev1) / k
 
-    ev0 = torch.cuda.Event(enable_timing=True)
-    ev1 = torch.cuda.Event(enable_timing=True)
-    barrier()
-    sync()
-    t0 = time.perf_counter()
-    ev0.record(stream)
-    for _ in range(args.steps):
-        step()
-    ev1.record(stream)
-    sync()
-    barrier()
-    t1 = time.perf_counter()
-    elapsed = t1 - t0
-    kernel_ms = ev0.elapsed_time(ev1) / args.steps  # launches back-to-back on `stream`
+    def alloc(self, nbytes):
+        """A device region on every rank, or None on every rank when any rank
+        cannot allocate (agreed before any other collective of the leg)."""
+        torch = self.torch
+        try:
+            region, err = torch.empty(nbytes, dtype=torch.uint8, device=self.dev), None
+        except torch.OutOfMemoryError as e:
+            region, err = None, str(e)
+        if not self.all_ok(region is not None):
+            del region
+            torch.cuda.empty_cache()
+            return None, err or "another rank could not allocate"
+        return region, None
 
-    elapsed_max = max_over_ranks(elapsed, device=dev)
 
-    total_bytes = bs * nb * world
-    value = total_bytes * args.steps / elapsed_max / 2**30
-    alg_bytes = nb * (bs + 4)  # block read + 4-byte CRC written (SURVEY §8d)
-    achieved = alg_bytes / (kernel_ms * 1e-3) / 1e9
-    traffic = load_traffic(bs, nb)
-    path = ctx.blocks_plan(region.data_ptr(), nb, bs)  # the library reports its own plan
-
-    result = {
-        "metric": METRIC,
-        "value": round(value, 2),
-        "unit": "GiB/s",
-        "n_gpus": world,
-        "steps": args.steps,
-        "warmup": args.warmup,
-        "ms_per_step": round(elapsed_max / args.steps * 1e3, 4),
-        "higher_is_better": True,
-        "scaling": "weak",
-        "vs_baseline": None,
-        "dtype": "u8",
-        "data": "synthetic (splitmix64 pattern filled on device)",
-        "config": {"workload": desc, "block_size": bs, "nblocks_per_gpu": nb,
-                   "bytes_per_gpu": bs * nb, "parallelism": f"shard{world} (contiguous block ranges, no collective)",
-                   "kernel": path, "untimed_ramp_launches": nramp, "untimed_ramp_s": round(ramp_s, 2),
-                   "also_measured": None if args.no_tib else CONFIGS["tib"][2] + " -> `tib`"},
-        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK_GBS, 4),
-                     "traffic": traffic, "kernel_ms": round(kernel_ms, 4),
-                     "alg_bytes_per_launch": alg_bytes},
-    }
-
-    if args.pipeline_streams > 1:
-        # Reported beside `value`, never instead of it: the same K batch
-        # passes, issued round-robin over independent streams as a server
-        # with several scrub/verify batches in flight would.  Kernels on one
-        # stream are serialized, so every batch pays its own tail;
-        # on separate streams the next batch's workgroups take the CUs that
-        # the previous one frees.  It gets the same untimed ramp as `value`.
-        ns = args.pipeline_streams
-        pstreams = [stream] + [torch.cuda.Stream(device=dev) for _ in range(ns - 1)]
-        pouts = [out] + [torch.empty(nb, dtype=torch.int32, device=dev) for _ in range(ns - 1)]
-
-        def pstep(i):
-            ctx.blocks_dev(region, bs, out=pouts[i % ns], stream=pstreams[i % ns])
-
-        ramp(pstep, stream, torch, window=2 * ns * 8, min_s=0.3)
-        sync()
-        barrier()
-        sync()
-        tp0 = time.perf_counter()
-        for i in range(args.steps):
-            pstep(i)
-        sync()
-        barrier()
-        p_elapsed = max_over_ranks(time.perf_counter() - tp0, device=dev)
-        same = all(torch.equal(pouts[0], o) for o in pouts[1:])
-        result["pipelined"] = {"streams": ns, "value": round(total_bytes * args.steps / p_elapsed / 2**30, 2),
-                               "unit": "GiB/s", "ms_per_step": round(p_elapsed / args.steps * 1e3, 4),
-                               "frac_of_peak": round(alg_bytes * args.steps / p_elapsed / 1e9 / HBM_PEAK_GBS, 4),
-                               "outputs_identical": bool(same)}
-
-    # every rank checks a sample of its own shard against the oracle
-    # (untimed); the CPU baseline times the reference on rank 0's sample
-    sys.path.insert(0, os.path.join(ROOT, "tests"))
+def resident_leg(B: Bench, name, steps, parity="full"):
+    """A device-resident config (CONFIGS[name]) at this N: each rank's shard
+    of world x nb blocks, filled on the device, ramped, then `steps` timed
+    passes.  parity "full": every block of every shard against the oracle;
+    "sampled": first, last and every 4096th block."""
     import _oracle as O
-    want_cpu = rank == 0 and not args.no_cpu_baseline
-    nsamp = max(1, min(nb, (args.cpu_sample_bytes if want_cpu else 64 << 20) // bs))
-    host = region[: nsamp * bs].cpu().numpy()
-    gpu_crc = as_u32(out[:nsamp])
-    del region
-    torch.cuda.empty_cache()
-
-    if not args.no_tib:
-        result["tib"] = tib_leg(args, torch, ctx, dev, rank, world, barrier, O)
-
-    # cold pass, LAST on the GPU: the device idles COLD_IDLE_S and ONE full
-    # pass over a fresh region of the same shape is timed -- what a one-off
-    # recovery scrub sees (clock ramp included).  Measured last so that the
-    # idle cannot leave its slower first launches inside the other legs.
-    cold_ms = cold_pass(torch, ctx, dev, bs, nb, stream)
-    result["cold_ms"] = round(cold_ms, 4)
-    result["cold"] = {"ms": round(cold_ms, 4), "value": round(bs * nb / (cold_ms * 1e-3) / 2**30, 2), "unit": "GiB/s",
-                      "note": f"rank-local first pass after {COLD_IDLE_S:.1f} s idle (kernel already loaded), "
-                              f"measured after all other GPU work"}
-
-    ok = bool(np.array_equal(O.crc32_blocks(host, bs, nthreads=8), gpu_crc))
-    all_ok = max_over_ranks(0.0 if ok else 1.0, device=dev) == 0.0
-    result["parity"] = {"checked_blocks_per_rank": nsamp, "bit_exact": bool(all_ok), "oracle": "oracle/crc_oracle.c"}
-    if want_cpu:
-        result["cpu_baseline"], cpu_ok = cpu_baseline(O, host, bs, gpu_crc)
-        result["parity"]["bit_exact_vs_reference_build"] = cpu_ok
-    barrier()
-    if rank == 0:
-        print(json.dumps(result), flush=True)
-    if world > 1:
-        dist.destroy_process_group()
-
-
-def cold_pass(torch, ctx, dev, bs, nb, stream):
-    """One full pass after the device has idled COLD_IDLE_S (fresh region of
-    the same shape, so nothing is cache-warm)."""
-    region = torch.empty(bs * nb, dtype=torch.uint8, device=dev)
-    ctx.fill_splitmix(region, SEED ^ 0xC01D)
-    out = torch.empty(nb, dtype=torch.int32, device=dev)
-    ctx.blocks_dev(region, bs, out=out, stream=stream, nblocks=min(nb, 64))
-    torch.cuda.synchronize()
-    time.sleep(COLD_IDLE_S)
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record(stream)
-    ctx.blocks_dev(region, bs, out=out, stream=stream)
-    e1.record(stream)
-    torch.cuda.synchronize()
-    del region, out
-    torch.cuda.empty_cache()
-    return e0.elapsed_time(e1)
-
-
-def tib_leg(args, torch, ctx, dev, rank, world, barrier, O):
-    """BASELINE configs[3]: this rank's 2 Mi x 64 KiB (128 GiB) shard of the
-    16 Mi x 64 KiB region (world ranks x 2 Mi blocks), filled on the device."""
     from priskv_amd import as_u32
-    from priskv_amd.shard import max_over_ranks, shard_blocks, shard_word_offset
-    bs = TIB_BS
-    first, nb = shard_blocks(world * TIB_NB, rank, world)
-    try:
-        region = torch.empty(bs * nb, dtype=torch.uint8, device=dev)
-    except torch.OutOfMemoryError as e:  # reported, never silently shrunk
-        return {"skipped": f"cannot allocate {bs * nb / 2**30:.0f} GiB: {e}"}
+    from priskv_amd.shard import shard_blocks, shard_word_offset
+    torch, ctx = B.torch, B.ctx
+    bs, nb0, desc = CONFIGS[name]
+    first, nb = shard_blocks(B.world * nb0, B.rank, B.world)
+    region, err = B.alloc(bs * nb)
+    if region is None:
+        return {"workload": desc, "skipped": f"cannot allocate {bs * nb / 2**30:.0f} GiB: {err}"}
     ctx.fill_splitmix(region, SEED, word_offset=shard_word_offset(first, bs))
-    out = torch.empty(nb, dtype=torch.int32, device=dev)
-    stream = torch.cuda.Stream(device=dev)
+    out = torch.empty(nb, dtype=torch.int32, device=B.dev)
+    stream = torch.cuda.Stream(device=B.dev)
 
-    def step(_i=0):
+    def step():
         ctx.blocks_dev(region, bs, out=out, stream=stream)
 
     step()
     torch.cuda.synchronize()
-    ramp(step, stream, torch, window=3, min_s=0.5)
-    k = max(1, args.tib_steps)
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    ev0.record(stream)
-    for _ in range(k):
-        step()
-    ev1.record(stream)
-    torch.cuda.synchronize()
-    barrier()
-    el = max_over_ranks(time.perf_counter() - t0, device=dev)
-    kms = ev0.elapsed_time(ev1) / k
-    # sampled parity: first and last block of the shard and every 4096th
-    # (the >2 GiB and >64 GiB ends of the shard included)
-    idx = np.unique(np.concatenate([np.arange(0, nb, 4096), [nb - 1]])).astype(np.int64)
-    ti = torch.from_numpy(idx).to(dev)
-    blocks = region.view(nb, bs).index_select(0, ti).cpu().numpy()
-    got = as_u32(out.index_select(0, ti))
-    want = O.crc32_blocks(blocks.reshape(-1), bs, nthreads=8)
-    ok = bool(np.array_equal(got, want))
-    all_ok = max_over_ranks(0.0 if ok else 1.0, device=dev) == 0.0
+    ramp(step, stream, torch, window=max(3, min(16, (64 << 30) // (bs * nb))), min_s=0.5)
+    k = max(1, steps)
+    el, kms = B.timed(step, stream, k)
+    if parity == "full":
+        host = region.cpu().numpy()
+        got = as_u32(out)
+        want = O.crc32_blocks(host, bs, nthreads=8)
+        nchk, what = nb, "every block"
+        del host
+    else:
+        idx = np.unique(np.concatenate([np.arange(0, nb, 4096), [nb - 1]])).astype(np.int64)
+        ti = torch.from_numpy(idx).to(B.dev)
+        blocks = region.view(nb, bs).index_select(0, ti).cpu().numpy()
+        got = as_u32(out.index_select(0, ti))
+        want = O.crc32_blocks(blocks.reshape(-1), bs, nthreads=8)
+        nchk, what = int(idx.size), "first, last, every 4096th block"
+    ok = B.all_ok(bool(np.array_equal(got, want)))
     alg = nb * (bs + 4)
     plan = ctx.blocks_plan(region.data_ptr(), nb, bs)
     del region, out
     torch.cuda.empty_cache()
-    return {"workload": CONFIGS["tib"][2], "value": round(bs * nb * world * k / el / 2**30, 2), "unit": "GiB/s",
-            "n_gpus": world, "steps": k, "ms_per_step": round(el / k * 1e3, 4), "bytes_per_gpu": bs * nb,
-            "kernel": plan, "roofline": {"achieved": round(alg / (kms * 1e-3) / 1e9, 1),
-                                                      "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                                                      "frac": round(alg / (kms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-                                                      "kernel_ms": round(kms, 4)},
-            "parity": {"checked_blocks_per_rank": int(idx.size), "sample": "first, last, every 4096th block",
-                       "bit_exact": bool(all_ok)}}
+    achieved = alg / (kms * 1e-3) / 1e9
+    return {"workload": desc, "value": round(bs * nb * B.world * k / el / 2**30, 2), "unit": "GiB/s",
+            "n_gpus": B.world, "steps": k, "ms_per_step": round(el / k * 1e3, 4), "bytes_per_gpu": bs * nb,
+            "kernel": plan,
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "kernel_ms": round(kms, 4),
+                         "alg_bytes_per_launch": alg},
+            "parity": {"checked_blocks_per_rank": nchk, "sample": what, "bit_exact": ok,
+                       "oracle": "oracle/crc_oracle.c"}}
+
+
+def streamed_leg(B: Bench, host, bs, want):
+    """configs[4]: this rank's headline blocks from host memory, end to end
+    through priskv_crc32_blocks_host (64 MiB chunks over 3 streams: H2D copy,
+    kernel and D2H of the CRCs overlapped).  Pinned = the region registered
+    with priskv_crc_host_register, as the server's RDMA-registered value
+    buffer / memfile would be; pageable = bounced through pinned staging.
+    `want` = the oracle's CRCs of `host`."""
+    from priskv_amd import host_register, host_unregister
+    nb = host.size // bs
+    res = {}
+    for mode in ("pinned", "pageable"):
+        if mode == "pinned":
+            host_register(host)
+        try:
+            out = B.ctx.blocks_host(host, bs)  # warm (allocates the staging buffers)
+            k = max(1, B.args.streamed_steps if mode == "pinned" else max(1, B.args.streamed_steps // 2))
+            B.barrier()
+            t0 = time.perf_counter()
+            for _ in range(k):
+                out = B.ctx.blocks_host(host, bs, out=out)
+            dt = B.max(time.perf_counter() - t0) / k
+            B.barrier()
+        finally:
+            if mode == "pinned":
+                host_unregister(host)
+        ok = B.all_ok(bool(np.array_equal(out, want)))
+        link = (nb * bs + nb * 4) / dt / 1e9  # bytes over this GPU's host link per second
+        res[mode] = {"value": round(bs * nb * B.world / dt / 2**30, 2), "unit": "GiB/s", "steps": k,
+                     "ms_per_step": round(dt * 1e3, 3),
+                     "roofline": {"bound": "pcie", "achieved": round(link, 2), "peak": PCIE_PEAK_GBS, "unit": "GB/s",
+                                  "frac": round(link / PCIE_PEAK_GBS, 4),
+                                  "peak_source": "PCIe Gen5 x16 host link spec, MI355X_MICROARCH.md"},
+                     "bit_exact": ok}
+    return {"workload": f"{nb} x {bs} B value blocks per GPU in host memory (BASELINE configs[4]): "
+                        f"H2D + kernel + D2H of the CRCs, 64 MiB chunks on 3 streams",
+            "n_gpus": B.world, **res,
+            "parity": {"checked_blocks_per_rank": nb, "sample": "every block, against the oracle",
+                       "bit_exact": res["pinned"]["bit_exact"] and res["pageable"]["bit_exact"]}}
+
+
+def cold_leg(B: Bench, bs, nb, walked):
+    """The first full pass after the device has idled COLD_IDLE_S: over a
+    fresh region (filled on the device, never hashed -- what a one-off
+    recovery scrub sees) and over `walked`, a region hashed many times
+    already.  Rank-local, measured after all other GPU work."""
+    torch, ctx = B.torch, B.ctx
+    stream = torch.cuda.Stream(device=B.dev)
+    out = torch.empty(nb, dtype=torch.int32, device=B.dev)
+    region = torch.empty(bs * nb, dtype=torch.uint8, device=B.dev)
+    ctx.fill_splitmix(region, SEED ^ 0xC01D)
+    ctx.blocks_dev(region, bs, out=out, stream=stream, nblocks=min(nb, 64))
+    res = {}
+    for label, reg in (("fresh", region), ("walked", walked)):
+        torch.cuda.synchronize()
+        time.sleep(COLD_IDLE_S)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        ctx.blocks_dev(reg, bs, out=out, stream=stream)
+        e1.record(stream)
+        torch.cuda.synchronize()
+        res[label] = e0.elapsed_time(e1)
+    del region, out
+    torch.cuda.empty_cache()
+    alg = nb * (bs + 4)
+    f = res["fresh"]
+    return {"ms": round(f, 4), "value": round(bs * nb / (f * 1e-3) / 2**30, 2), "unit": "GiB/s",
+            "frac": round(alg / (f * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+            "walked_ms": round(res["walked"], 4),
+            "walked_value": round(bs * nb / (res["walked"] * 1e-3) / 2**30, 2),
+            "note": f"rank-local first pass after {COLD_IDLE_S:.1f} s idle over a fresh region (filled, never "
+                    f"hashed) and, walked_*, over the headline region (hashed many times); kernel already loaded; "
+                    f"measured after all other GPU work"}
 
 
 def cpu_baseline(O, host, bs, gpu_crc):
@@ -426,34 +409,150 @@ def cpu_model():
     return "unknown"
 
 
-def streamed(args, torch, rank, world):
-    """BASELINE config 5: 4 KiB blocks from pinned host memory, end to end."""
-    from priskv_amd import CrcContext, host_register, host_unregister
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    rehearsal = os.environ.get("PRISKV_BENCH_REHEARSAL", "") == "1"
+    if world != args.gpus and rank == 0:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+    # device_count() does not initialise the GPU on this image: the guard
+    # runs before any HIP call
+    ndev = torch.cuda.device_count()
+    why = device_guard(world, local, ndev, rehearsal)
+    if why:
+        print(f"bench.py: rank {rank}: {why}", file=sys.stderr, flush=True)
+        sys.exit(EXIT_DEVICES)
+    gpu = local % ndev if rehearsal else local
+    torch.cuda.set_device(gpu)
+    dev = torch.device("cuda", gpu)
+    backend = os.environ.get("PRISKV_BENCH_BACKEND", "gloo" if rehearsal else "nccl")  # nccl == RCCL on ROCm
+    if world > 1:
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
+    infos = gather_obj(device_info(torch, rank, local, gpu), world)
+    dups = duplicate_devices(infos)
+    if dups and not rehearsal:
+        if rank == 0:
+            print(f"bench.py: ranks share a physical device: {dups}", file=sys.stderr, flush=True)
+        if world > 1:
+            dist.destroy_process_group()
+        sys.exit(EXIT_DEVICES)
+
+    from priskv_amd import CrcContext, as_u32
+    from priskv_amd.shard import shard_blocks, shard_word_offset
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import _oracle as O
-    bs = args.block_size or 4096
-    nb = args.nblocks or (1 << 20)
-    ctx = CrcContext(int(os.environ.get("LOCAL_RANK", "0")))
-    host = O.fill_splitmix(bs * nb, SEED, rank * (bs * nb // 8))
-    res = {}
-    for mode in ("pinned", "pageable"):
-        if mode == "pinned":
-            host_register(host)
-        out = ctx.blocks_host(host, bs)  # warm (allocates staging)
-        t0 = time.perf_counter()
-        for _ in range(args.steps):
-            out = ctx.blocks_host(host, bs)
-        dt = (time.perf_counter() - t0) / args.steps
-        if mode == "pinned":
-            host_unregister(host)
-        res[mode] = round(bs * nb / dt / 2**30, 2)
-    samp = min(nb, 65536)
-    ok = bool(np.array_equal(out[:samp], O.crc32_blocks(host[: samp * bs], bs, nthreads=8)))
-    print(json.dumps({"metric": "GiB/s CRC of host-resident value blocks (PCIe-inclusive, streamed)",
-                      "value": res["pinned"], "unit": "GiB/s", "n_gpus": 1, "steps": args.steps,
-                      "pageable_GiBs": res["pageable"], "config": {"workload": f"{nb} x {bs} B host blocks",
-                                                                   "block_size": bs},
-                      "parity": {"checked_blocks": samp, "bit_exact": ok}}), flush=True)
+
+    bs, nb, desc = CONFIGS[args.config]
+    if args.block_size:
+        bs = args.block_size
+    if args.nblocks:
+        nb = args.nblocks
+    ctx = CrcContext(gpu)
+    B = Bench(args, torch, dist, world, rank, dev, ctx)
+    # weak scaling: the global region has world * nb blocks; this rank's shard
+    # is its contiguous range of them (no data-path collective)
+    first, nb = shard_blocks(world * nb, rank, world)
+    region = torch.empty(bs * nb, dtype=torch.uint8, device=dev)
+    ctx.fill_splitmix(region, SEED, word_offset=shard_word_offset(first, bs))
+    out = torch.empty(nb, dtype=torch.int32, device=dev)
+    # a created stream: torch's null stream costs ~1 % per launch (DESIGN.md
+    # §6); the device-wide synchronize() around the timed region covers every
+    # stream
+    stream = torch.cuda.Stream(device=dev)
+
+    def step():
+        ctx.blocks_dev(region, bs, out=out, stream=stream)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    nramp, ramp_s = ramp(step, stream, torch)
+
+    elapsed_max, kernel_ms = B.timed(step, stream, args.steps)
+
+    total_bytes = bs * nb * world
+    value = total_bytes * args.steps / elapsed_max / 2**30
+    alg_bytes = nb * (bs + 4)  # block read + 4-byte CRC written (SURVEY §8d)
+    achieved = alg_bytes / (kernel_ms * 1e-3) / 1e9
+    traffic = load_traffic(bs, nb)
+    path = ctx.blocks_plan(region.data_ptr(), nb, bs)  # the library reports its own plan
+
+    result = {
+        "metric": METRIC,
+        "value": round(value, 2),
+        "unit": "GiB/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed_max / args.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic (splitmix64 pattern filled on device)",
+        "config": {"workload": desc, "block_size": bs, "nblocks_per_gpu": nb,
+                   "bytes_per_gpu": bs * nb, "parallelism": f"shard{world} (contiguous block ranges, no collective)",
+                   "kernel": path, "untimed_ramp_launches": nramp, "untimed_ramp_s": round(ramp_s, 2),
+                   "timed_launches": f"dispatches {args.warmup + nramp + 1}..{args.warmup + nramp + args.steps} of "
+                                     f"this kernel in the process (1-based; tools/ktrace_window.py)"},
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBS, 4),
+                     "traffic": traffic, "kernel_ms": round(kernel_ms, 4),
+                     "alg_bytes_per_launch": alg_bytes},
+    }
+
+    # the whole shard to host (untimed): every block is checked against the
+    # oracle, rank 0's first cpu-sample-bytes time the CPU baseline, and the
+    # streamed leg reads these same bytes from host memory
+    host = region.cpu().numpy()
+    gpu_crc = as_u32(out)
+    want = O.crc32_blocks(host, bs, nthreads=8)
+    head_ok = B.all_ok(bool(np.array_equal(gpu_crc, want)))
+    walked = region if args.config == "default" else None
+    if walked is None:
+        del region
+    del out
+    torch.cuda.empty_cache()
+
+    if not args.no_sweep and args.config == "default":
+        result["sweep"] = {k: resident_leg(B, name, args.sweep_steps) for k, name in SWEEP}
+    if not args.no_tib and args.config == "default":
+        result["tib"] = resident_leg(B, "tib", args.tib_steps, parity="sampled")
+    if not args.no_streamed:
+        result["streamed"] = streamed_leg(B, host, bs, want)
+    # cold passes LAST on the GPU: what a one-off recovery scrub sees (clock
+    # ramp included); measured last so that the idle cannot leave its slower
+    # first launches inside the other legs
+    if walked is not None:
+        result["cold"] = cold_leg(B, bs, nb, walked)
+        result["cold_ms"] = result["cold"]["ms"]
+        del walked
+    torch.cuda.empty_cache()
+
+    kms = gather_obj(round(kernel_ms, 4), world)
+    result["ranks"] = [dict(i, kernel_ms=k) for i, k in zip(infos, kms)]
+    result["dist"] = {"backend": dist.get_backend() if world > 1 else None, "world_size": world,
+                      "distinct_devices": len({(i["host"], i["pci"] or i["uuid"]) for i in infos}),
+                      "rehearsal": rehearsal}
+    result["parity"] = {"checked_blocks_per_rank": nb, "sample": "every block", "bit_exact": head_ok,
+                        "oracle": "oracle/crc_oracle.c"}
+    if rank == 0 and not args.no_cpu_baseline:
+        nsamp = max(1, min(nb, args.cpu_sample_bytes // bs))
+        result["cpu_baseline"], cpu_ok = cpu_baseline(O, host[: nsamp * bs], bs, gpu_crc[:nsamp])
+        result["parity"]["bit_exact_vs_reference_build"] = cpu_ok
+    B.barrier()
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
 
 
 if __name__ == "__main__":

@@ -176,15 +176,19 @@ const char *priskv_crc32_host_impl(void);
 int priskv_crc_fill_splitmix_dev(const priskv_crc_ctx *ctx, void *d_dst, uint64_t nbytes,
                                  uint64_t seed, uint64_t word_offset, void *stream);
 
-/* Which kernel a (d_base, block_size) batch dispatches to: 1 = rows (block
- * a multiple of 1 KiB, 16-byte aligned base: G = 16/32/64 lanes per block;
- * batches of few large blocks are hashed as segments and combined),
- * 3 = sub-KiB power-of-two blocks (16-byte aligned base), 5 = uniform stride
- * (any other block >= 16 B at any base alignment: rows aligned to each
- * block's end; few large unbalanced blocks are cut into segments), 4 =
- * generic (blocks below 16 B: one thread per block).  2 = extents is what a
- * context created with PRISKV_CRC_STRIDE=0 uses instead of 5 from 1 KiB (and
- * 4 below).  For tests and benchmarks; -EINVAL for invalid arguments. */
+/* Which kernel family a (d_base, block_size) batch dispatches to on a
+ * context with default options: 1 = rows (block a multiple of 1 KiB,
+ * 16-byte aligned base: G = 16/32/64 lanes per block; batches of few large
+ * blocks are hashed as segments and combined), 3 = sub-KiB power-of-two
+ * blocks (16-byte aligned base), 5 = uniform stride (any other block of
+ * 16 B up to 4.5 KiB when the size or base is not a multiple of 4, up to
+ * 9 KiB otherwise: rows aligned to each block's end), 2 = extents (the
+ * larger such blocks, and every block beyond 64 MiB), 4 = generic (blocks
+ * below 16 B: one thread per block).  Context options (PRISKV_CRC_STRIDE=0,
+ * PRISKV_CRC_STRIDE_MAX_KIB) move the 5 / 2 boundary; the exact kernels a
+ * given context launches, few-block segmentation included, are reported by
+ * priskv_crc32_blocks_plan.  For tests and benchmarks; -EINVAL for invalid
+ * arguments. */
 int priskv_crc32_blocks_path(const void *d_base, uint64_t nblocks, uint32_t block_size);
 
 /* The kernel plan priskv_crc32_blocks_dev would launch for this batch on

@@ -771,11 +771,25 @@ constexpr uint32_t kStrideMaxBlock = 64u << 20; // larger odd blocks keep the (s
 constexpr uint32_t kStrideOddMax = 4608;
 constexpr uint32_t kStrideMax = 9u << 10;
 
-bool stride_to_extents(const priskv_crc_ctx *ctx, const void *base, uint32_t bs)
+bool stride_to_extents_lim(const void *base, uint32_t bs, uint64_t odd_max, uint64_t max, bool funnel)
 {
     const bool odd = (((uintptr_t)base | bs) & 3u) != 0;
-    return bs > kStrideMaxBlock || (odd && bs >= ctx->stride_odd_max && ctx->stride_funnel) ||
-           (!odd && bs >= ctx->stride_max);
+    return bs > kStrideMaxBlock || (odd && bs >= odd_max && funnel) || (!odd && bs >= max);
+}
+
+bool stride_to_extents(const priskv_crc_ctx *ctx, const void *base, uint32_t bs)
+{
+    return stride_to_extents_lim(base, bs, ctx->stride_odd_max, ctx->stride_max, ctx->stride_funnel);
+}
+
+// the extents-path kernels a batch of n extents of at most max_len bytes
+// launches (max_len 0: lengths on the device)
+const char *extents_desc(const priskv_crc_ctx *ctx, uint64_t n, uint64_t max_len)
+{
+    if (!extents_segmented(ctx, n, max_len))
+        return "crc_ranges_kernel (extents)";
+    return ctx->fused ? "crc_ranges_fused_kernel (few large values: segments, one launch)"
+                      : "crc_seg_plan_kernel + crc_ranges_kernel (segments) + crc_seg_reduce_kernel";
 }
 
 StridePlan stride_plan(const priskv_crc_ctx *ctx, uint32_t bs)
@@ -1002,7 +1016,12 @@ int priskv_crc32_blocks_path(const void *d_base, uint64_t nblocks, uint32_t bloc
 {
     if (block_size == 0 || (nblocks && !d_base))
         return -EINVAL;
-    return choose_path(d_base, block_size);
+    const int path = choose_path(d_base, block_size);
+    // a default context sends odd blocks from 4.5 KiB, other stride sizes
+    // from 9 KiB and blocks beyond 64 MiB to the extents kernel
+    if (path == PATH_STRIDE && stride_to_extents_lim(d_base, block_size, kStrideOddMax, kStrideMax, true))
+        return PATH_EXTENTS;
+    return path;
 }
 
 int priskv_crc32_blocks_plan(const priskv_crc_ctx *ctx, const void *d_base, uint64_t nblocks, uint32_t block_size,
@@ -1016,8 +1035,7 @@ int priskv_crc32_blocks_plan(const priskv_crc_ctx *ctx, const void *d_base, uint
     if (path == PATH_STRIDE) {
         const StridePlan P = stride_plan(ctx, block_size);
         if (stride_to_extents(ctx, d_base, block_size)) {
-            w = snprintf(buf, len, "%s", extents_segmented(ctx, nblocks, block_size) && ctx->fused ? fused_name
-                                                                                                   : "crc_ranges_kernel (extents)");
+            w = snprintf(buf, len, "%s", extents_desc(ctx, nblocks, block_size));
         } else if (stride_segmented(ctx, P, nblocks, block_size)) {
             w = snprintf(buf, len, "%s", fused_name);
         } else {
@@ -1053,11 +1071,7 @@ int priskv_crc32_blocks_plan(const priskv_crc_ctx *ctx, const void *d_base, uint
     } else if (path == PATH_SMALL) {
         w = snprintf(buf, len, "crc_small_kernel<G=%u>", block_size / 16);
     } else if (path == PATH_EXTENTS) {
-        const bool seg = extents_segmented(ctx, nblocks, block_size);
-        w = snprintf(buf, len, "%s", !seg ? "crc_ranges_kernel (extents)"
-                                          : (ctx->fused ? fused_name
-                                                        : "crc_seg_plan_kernel + crc_ranges_kernel (segments) + "
-                                                          "crc_seg_reduce_kernel"));
+        w = snprintf(buf, len, "%s", extents_desc(ctx, nblocks, block_size));
     } else {
         w = snprintf(buf, len, "crc_generic_kernel");
     }
@@ -1371,57 +1385,105 @@ bool host_mapped(const void *h, uint64_t len, void **dptr)
 
 // Registrations this library makes on the caller's behalf (the zero-copy
 // scrub of a region the caller did not register).  One process-wide registry
-// keyed by base: concurrent calls over the same region -- several GPUs
-// scrubbing one memfile, the batcher beside a scrub -- share one
-// registration, and the last user unregisters it.  Check, register and
-// refcount happen under one lock, so no caller can see another's temporary
-// mapping disappear while its kernel still reads it.
+// of byte ranges: a call whose range lies inside a live temporary
+// registration -- several GPUs scrubbing one memfile, the batcher beside a
+// scrub, a scrub of a sub-range -- takes a reference on that registration,
+// and the last user unregisters it.  A call whose range overlaps a live
+// temporary registration without lying inside it waits until that
+// registration is gone and then registers its own (pages cannot be
+// registered twice).  A caller never waits while it holds a reference, so
+// the wait always ends; a new caller whose range overlaps a waiting one
+// queues behind it, so a caller that scrubs in a loop cannot keep a waiter
+// out.  Check, register and refcount happen under one lock, so no caller can
+// see a temporary mapping it reads through disappear.
 struct TempReg {
-    const void *base;
+    const uint8_t *base;
     uint64_t len;
     int refs;
 };
 pthread_mutex_t g_reg_lock = PTHREAD_MUTEX_INITIALIZER;
+pthread_cond_t g_reg_gone = PTHREAD_COND_INITIALIZER;
 std::vector<TempReg> g_regs;
+std::vector<TempReg> g_reg_waiters; // ranges of callers waiting in reg_acquire (refs unused)
 
-// *dptr = device view of [base, base + len); *held = a registry reference
-// was taken (release it with reg_release)
-int reg_acquire(const void *base, uint64_t len, void **dptr, bool *held)
+bool ranges_overlap(const uint8_t *a, uint64_t alen, const uint8_t *b, uint64_t blen)
 {
-    *held = false;
+    return a < b + blen && b < a + alen;
+}
+
+// a waiter leaves the queue: new callers it held back may go
+void reg_unwait(const uint8_t *b, uint64_t len)
+{
+    for (size_t i = 0; i < g_reg_waiters.size(); i++)
+        if (g_reg_waiters[i].base == b && g_reg_waiters[i].len == len) {
+            g_reg_waiters.erase(g_reg_waiters.begin() + (ptrdiff_t)i);
+            pthread_cond_broadcast(&g_reg_gone);
+            return;
+        }
+}
+
+// *dptr = device view of [base, base + len); *reg = the temporary
+// registration a reference was taken on (release it with reg_release), or
+// nullptr when the range is the caller's own registration / pinned memory
+int reg_acquire(const void *base, uint64_t len, void **dptr, const void **reg)
+{
+    *reg = nullptr;
+    const uint8_t *b = static_cast<const uint8_t *>(base);
     pthread_mutex_lock(&g_reg_lock);
-    int rc = 0;
-    for (TempReg &r : g_regs) {
-        if (r.base != base)
-            continue;
-        if (r.len < len) {
-            rc = -EBUSY; // a shorter temporary mapping of the same base is in use
-        } else {
-            r.refs++;
-            *held = true;
-            if (!host_mapped(base, len, dptr))
+    bool waiting = false;
+    for (;;) {
+        const TempReg *cover = nullptr;
+        bool blocked = false;
+        for (const TempReg &r : g_regs) {
+            if (b >= r.base && (uint64_t)(b - r.base) <= r.len && len <= r.len - (uint64_t)(b - r.base))
+                cover = &r;
+            else if (ranges_overlap(b, len, r.base, r.len))
+                blocked = true;
+        }
+        if (cover) {
+            int rc = 0;
+            if (host_mapped(base, len, dptr)) {
+                const_cast<TempReg *>(cover)->refs++;
+                *reg = cover->base;
+            } else {
                 rc = -EIO;
+            }
+            if (waiting)
+                reg_unwait(b, len);
+            pthread_mutex_unlock(&g_reg_lock);
+            return rc;
         }
-        if (rc && *held) {
-            r.refs--;
-            *held = false;
+        if (!blocked && !waiting)
+            for (const TempReg &w : g_reg_waiters)
+                blocked |= ranges_overlap(b, len, w.base, w.len);
+        if (!blocked)
+            break;
+        if (!waiting) {
+            try {
+                g_reg_waiters.push_back(TempReg{b, len, 0});
+            } catch (...) {
+                pthread_mutex_unlock(&g_reg_lock);
+                return -ENOMEM;
+            }
+            waiting = true;
         }
-        pthread_mutex_unlock(&g_reg_lock);
-        return rc;
+        pthread_cond_wait(&g_reg_gone, &g_reg_lock);
     }
+    if (waiting)
+        reg_unwait(b, len);
     if (host_mapped(base, len, dptr)) { // the caller's own registration / pinned memory
         pthread_mutex_unlock(&g_reg_lock);
         return 0;
     }
-    rc = herr(hipHostRegister(const_cast<void *>(base), len, hipHostRegisterPortable | hipHostRegisterMapped));
+    int rc = herr(hipHostRegister(const_cast<void *>(base), len, hipHostRegisterPortable | hipHostRegisterMapped));
     if (!rc && !host_mapped(base, len, dptr)) {
         (void)hipHostUnregister(const_cast<void *>(base));
         rc = -EIO;
     }
     if (!rc) {
         try {
-            g_regs.push_back(TempReg{base, len, 1});
-            *held = true;
+            g_regs.push_back(TempReg{b, len, 1});
+            *reg = b;
         } catch (...) {
             (void)hipHostUnregister(const_cast<void *>(base));
             rc = -ENOMEM;
@@ -1431,15 +1493,18 @@ int reg_acquire(const void *base, uint64_t len, void **dptr, bool *held)
     return rc;
 }
 
-void reg_release(const void *base)
+void reg_release(const void *reg)
 {
+    if (!reg)
+        return;
     pthread_mutex_lock(&g_reg_lock);
     for (size_t i = 0; i < g_regs.size(); i++) {
-        if (g_regs[i].base != base)
+        if (g_regs[i].base != reg)
             continue;
         if (--g_regs[i].refs == 0) {
-            (void)hipHostUnregister(const_cast<void *>(base));
+            (void)hipHostUnregister(const_cast<uint8_t *>(g_regs[i].base));
             g_regs.erase(g_regs.begin() + (ptrdiff_t)i);
+            pthread_cond_broadcast(&g_reg_gone);
         }
         break;
     }
@@ -1468,8 +1533,8 @@ int priskv_crc32_ranges_host(priskv_crc_ctx *ctx, const void *h_base, uint64_t r
     // device view of the host mapping (zero-copy): the caller's registration
     // or pinned memory, else a shared temporary registration (reg_acquire)
     void *dptr = nullptr;
-    bool held = false;
-    if (int rc = reg_acquire(h_base, region_bytes, &dptr, &held))
+    const void *reg = nullptr;
+    if (int rc = reg_acquire(h_base, region_bytes, &dptr, &reg))
         return rc;
     pthread_mutex_lock(&ctx->lock);
     int rc = 0;
@@ -1494,8 +1559,7 @@ int priskv_crc32_ranges_host(priskv_crc_ctx *ctx, const void *h_base, uint64_t r
             (void)hipStreamSynchronize(ctx->aux);
     }
     pthread_mutex_unlock(&ctx->lock);
-    if (held)
-        reg_release(h_base);
+    reg_release(reg);
     return rc;
 }
 
@@ -1612,12 +1676,11 @@ int priskv_crc32_ranges_host_multi(priskv_crc_ctx *const *ctxs, int nctx, const 
     // one shared registration for all devices (the per-shard calls then find
     // it in the registry instead of each registering the range)
     void *probe = nullptr;
-    bool held = false;
-    if (int rc = reg_acquire(h_base, region_bytes, &probe, &held))
+    const void *reg = nullptr;
+    if (int rc = reg_acquire(h_base, region_bytes, &probe, &reg))
         return rc;
     const int rc = run_multi(ctxs, nctx, p, n);
-    if (held)
-        reg_release(h_base);
+    reg_release(reg);
     return rc;
 }
 

@@ -1059,6 +1059,55 @@ def test_ranges_host_concurrent_temporary_registration(torch_cuda):
     host_unregister(region)
 
 
+def test_ranges_host_overlapping_subranges(torch_cuda):
+    """Three threads scrub views of one unregistered region: the whole
+    region, its first 20 MiB and everything from 12 MiB on (views with other
+    base pointers, which overlap each other without either containing the
+    other).  A view inside a live temporary registration must take a
+    reference on it (else the owner's unregister pulls the mapping from
+    under the view's kernel), and an overlapping view must wait for it
+    instead of failing.  No registration may leak."""
+    import threading
+    from priskv_amd import CrcContext, host_register, host_unregister
+    region = O.fill_splitmix(32 << 20, SEED, 47)
+    views = [(0, region.size), (0, 20 << 20), (12 << 20, region.size)]
+    rng = np.random.default_rng(47)
+    jobs = []
+    for t, (a, b) in enumerate(views):
+        v = region[a:b]
+        for _ in range(10):
+            lens = rng.integers(0, 200000, 300).astype(np.uint32)
+            offs = np.array([rng.integers(0, v.size - int(ln)) for ln in lens], dtype=np.uint64)
+            jobs.append((t, offs, lens, O.crc32_ranges(v, offs, lens)))
+    ctxs = [CrcContext(0) for _ in views]
+    errors = []
+
+    def worker(t):
+        a, b = views[t]
+        v = region[a:b]
+        try:
+            for tt, offs, lens, want in jobs:
+                if tt != t:
+                    continue
+                got = ctxs[t].ranges_host(v, offs, lens)
+                if not np.array_equal(got, want):
+                    errors.append((t, "mismatch"))
+        except Exception as e:  # noqa: BLE001 -- reported below
+            errors.append((t, repr(e)))
+
+    th = [threading.Thread(target=worker, args=(t,)) for t in range(len(views))]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join(timeout=120)
+    assert not any(x.is_alive() for x in th), "a scrub never returned (registry wait)"
+    for c in ctxs:
+        c.close()
+    assert not errors, errors[:4]
+    host_register(region)  # would raise EEXIST if a temporary registration had leaked
+    host_unregister(region)
+
+
 def test_batcher_flush_while_others_submit(torch_cuda, ctx):
     """flush() returns only after every value its thread submitted before it
     has been called back, while other threads keep submitting (the gather

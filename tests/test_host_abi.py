@@ -230,6 +230,13 @@ def test_path_selection():
     assert C.blocks_path(4096, 10, 4100) == "stride"    # not a multiple of 1 KiB
     assert C.blocks_path(4096, 10, 1000) == "stride"
     assert C.blocks_path(4097, 10, 256) == "stride"     # sub-KiB power of two, unaligned base
+    # the default limits hand larger stride sizes to the extents kernel
+    assert C.blocks_path(4096, 10, 4607) == "stride"
+    assert C.blocks_path(4096, 10, 4609) == "extents"   # odd from 4.5 KiB
+    assert C.blocks_path(4097, 10, 8192) == "extents"   # unaligned base counts as odd
+    assert C.blocks_path(4096, 10, 9212) == "stride"
+    assert C.blocks_path(4096, 10, 9220) == "extents"   # multiples of 4 from 9 KiB
+    assert C.blocks_path(4096, 10, (64 << 20) + 4) == "extents"
     assert C.blocks_path(4096, 10, 15) == "generic"     # below one 16-B window
     assert C.blocks_path(4096, 10, 1) == "generic"
 

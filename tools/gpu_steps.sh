@@ -21,6 +21,9 @@
 #   ktrace[:A,B,...]      rocprofv3 --kernel-trace --stats over bench.py A B ...
 #   ktracepy:SCRIPT[:A,B] rocprofv3 --kernel-trace --stats over python tools/SCRIPT A B ...
 #   pmc:C1+C2[:A,B,...]   one rocprofv3 --pmc pass (counters C1 C2 ...) over bench.py A B ...
+#   pmcpy:C1+C2:SCRIPT[:A,B]  one --pmc pass over python tools/SCRIPT A B ...
+#   oversub               bench.py as 2 ranks on this one GPU WITHOUT the rehearsal
+#                         variable: must exit 3 (the device guard) -- the step fails otherwise
 set -euo pipefail
 R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
 TAG=$1
@@ -80,9 +83,20 @@ for step in "$@"; do
                 -- python3 "$R/bench.py" ${arg//,/ } > "$O/ktrace_$n.json" 2> "$O/ktrace_$n.err")
         ;;
     gloo2)
-        PRISKV_BENCH_BACKEND=gloo timeout -k 10 400 python -m torch.distributed.run --nnodes 1 --nproc-per-node 2 \
+        PRISKV_BENCH_REHEARSAL=1 timeout -k 10 400 python -m torch.distributed.run --nnodes 1 --nproc-per-node 2 \
             --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 2 ${arg//,/ } > "$O/gloo2_$n.json" \
             2> "$O/gloo2_$n.err"
+        ;;
+    oversub)
+        set +e
+        timeout -k 10 120 python -m torch.distributed.run --nnodes 1 --nproc-per-node 2 \
+            --master-addr 127.0.0.1 --master-port 29519 bench.py --gpus 2 --steps 2 --warmup 1 \
+            > "$O/oversub_$n.out" 2> "$O/oversub_$n.err"
+        rc=$?
+        set -e
+        echo "oversubscribed launch exit status $rc" >> "$O/oversub_$n.err"
+        [[ $rc -ne 0 && $rc -ne 124 && $rc -ne 137 ]]
+        grep -q "has no GPU of its own" "$O/oversub_$n.err"
         ;;
     ktracepy)
         script=${arg%%:*}
@@ -99,6 +113,17 @@ for step in "$@"; do
         (cd /tmp && export TMPDIR=/tmp &&
             timeout -s KILL 180 rocprofv3 --pmc ${ctrs//+/ } -d "$O/pmc_$n" -o run --output-format csv \
                 -- python3 "$R/bench.py" ${bargs//,/ } > "$O/pmc_$n.json" 2> "$O/pmc_$n.err")
+        ;;
+    pmcpy)
+        # pmcpy:C1+C2:SCRIPT[:A,B] -- one --pmc pass over python tools/SCRIPT A B ...
+        ctrs=${arg%%:*}
+        rest=${arg#*:}
+        script=${rest%%:*}
+        pargs=""
+        [[ "$rest" == *:* ]] && pargs=${rest#*:}
+        (cd /tmp && export TMPDIR=/tmp &&
+            timeout -s KILL 180 rocprofv3 --pmc ${ctrs//+/ } -d "$O/pmcpy_$n" -o run --output-format csv \
+                -- python3 "$R/tools/$script" ${pargs//,/ } > "$O/pmcpy_$n.out" 2> "$O/pmcpy_$n.err")
         ;;
     *)
         echo "unknown step $step" >&2
