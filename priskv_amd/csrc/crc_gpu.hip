@@ -71,6 +71,7 @@ struct priskv_crc_ctx {
     int segment;               // split few large blocks / extents into segments (PRISKV_CRC_SEGMENT=0: off)
     int prio;                  // rows kernel progress priority (PRISKV_CRC_PRIO=0: off)
     int balance;               // byte-balanced extents split (PRISKV_CRC_BALANCE=0: off)
+    int ext_adapt;             // per-wave chunk size of the many-extents shape (PRISKV_CRC_EXT_ADAPT=0: 2 rows)
     uint64_t seg_max_extents;  // device-resident lengths: segment calls of at most this many extents
     int xcd_rr;                // the XCD probe found workgroup b on XCD b % 8 (weights apply)
     uint64_t tile_min_bytes;   // rows batches of at least this many bytes run in block-cyclic tiles
@@ -298,9 +299,11 @@ constexpr int kExtRows = 2; // rows per chunk of the extents kernel (tools/range
 // per CU with progress-priority mode 3 (kExtOptMany: bits 8-9 and 10; the
 // progress slots do not fit beside two 80 KiB table sets in 160 KiB of LDS).
 // Many small values gain 5-7 %; a few large extents per wave lose 2-4 % in
-// the 16-wave shape, so they keep the first.
+// the 16-wave shape, so they keep the first.  In the 16-wave shape each wave
+// sizes its chunks (8, 4 or 2 rows) from its own extents (bit 14; scattered
+// values of 2-4 blocks +5-8 %, tools/ranges_explore, profiles/r03/ranges/).
 constexpr int kExtOpt = 3;
-constexpr int kExtOptMany = 3 | (3 << 8) | 1024;
+constexpr int kExtOptMany = 3 | (3 << 8) | 1024 | 16384;
 constexpr uint64_t kExtManyPerWave = 32; // extents per resident wave for kExtOptMany
 constexpr int kExtWaves = kWaves;         // kExtOpt's shape: waves per workgroup ...
 constexpr int kExtWgPerCu = 2;            // ... and workgroups per CU (the same 16 waves per CU)
@@ -330,8 +333,10 @@ int launch_ext_kernel(const priskv_crc_ctx *ctx, bool seg, bool many, bool bal, 
         fn = reinterpret_cast<const void *>(&crc_ranges_kernel<kExtRows, kNbuf, kAux, kExtOpt | 4>);
     else if (bal && !many)
         fn = reinterpret_cast<const void *>(&crc_ranges_kernel<kExtRows, kNbuf, kAux, kExtOpt | 2048>);
-    else if (many)
+    else if (many && ctx->ext_adapt)
         fn = reinterpret_cast<const void *>(&crc_ranges_kernel<kExtRows, kNbuf, kAux, kExtOptMany>);
+    else if (many)
+        fn = reinterpret_cast<const void *>(&crc_ranges_kernel<kExtRows, kNbuf, kAux, kExtOptMany & ~16384>);
     else
         fn = reinterpret_cast<const void *>(&crc_ranges_kernel<kExtRows, kNbuf, kAux, kExtOpt>);
     return herr(hipLaunchKernel(fn, dim3(grid ? grid : 1), dim3(64 * waves), args, 0, s));
@@ -1113,6 +1118,8 @@ int priskv_crc_ctx_create(int device, priskv_crc_ctx **out)
         c->prio = !(pe && !strcmp(pe, "0"));
         const char *be = getenv("PRISKV_CRC_BALANCE");
         c->balance = !(be && !strcmp(be, "0"));
+        const char *ea = getenv("PRISKV_CRC_EXT_ADAPT");
+        c->ext_adapt = !(ea && !strcmp(ea, "0"));
         const char *fe = getenv("PRISKV_CRC_FUSED");
         c->fused = !(fe && !strcmp(fe, "0"));
         const char *se = getenv("PRISKV_CRC_STRIDE");

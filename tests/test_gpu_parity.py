@@ -565,6 +565,46 @@ def test_ranges_many_per_wave_shapes(torch_cuda, any_ctx):
     assert np.array_equal(got, want), np.nonzero(got != want)[0][:8]
 
 
+def test_ranges_many_shape_chunk_sizes(torch_cuda, ctx):
+    """The 16-wave many-extents shape sizes each wave's chunks from its own
+    extents (8, 4 or 2 rows: crc_device.inc OPT bit 14).  Three populations
+    of 65 536 extents, each a contiguous index range so that its waves pick
+    one size: values of 2 blocks with ragged ends (8-row chunks), aligned
+    4096-B extents (4-row chunks) and short values of 0-1500 B (2-row
+    chunks); lengths around every 1 KiB row and 8 KiB chunk edge at all 16
+    start phases are spread over the first two.  Every extent against the
+    oracle, output pre-filled with a sentinel."""
+    torch = torch_cuda
+    n = 256 << 20
+    t = _region(torch, ctx, n, SEED, 51)
+    rng = np.random.default_rng(51)
+    m = 65536
+    nblk = n // 4096 - 8
+    o8 = rng.integers(0, nblk, m).astype(np.uint64) * 4096
+    l8 = (8192 - rng.integers(0, 4096, m)).astype(np.uint32)
+    edges = [(k * 1024 + d, ph) for k in (1, 2, 4, 7, 8, 9, 15, 16, 17) for d in (-17, -16, -1, 0, 1, 15, 16)
+             for ph in range(16)]
+    for j, (ln, ph) in enumerate(edges):  # chunk and row edges in the first population
+        l8[7 * j] = max(0, ln)
+        o8[7 * j] = o8[7 * j] + ph
+    o4 = rng.integers(0, nblk, m).astype(np.uint64) * 4096
+    l4 = np.full(m, 4096, dtype=np.uint32)
+    o2 = rng.integers(0, n - 2000, m).astype(np.uint64)
+    l2 = rng.integers(0, 1500, m).astype(np.uint32)
+    l2[:4] = [0, 1, 1024, 1499]
+    offs = np.concatenate([o8, o4, o2])
+    lens = np.concatenate([l8, l4, l2])
+    sentinel = int(np.int32(np.uint32(0xA5A5A5A5).view(np.int32)))
+    out = torch.full((3 * m,), sentinel, dtype=torch.int32, device="cuda")
+    ctx.ranges_dev(t, torch.from_numpy(offs.astype(np.int64)).cuda(), torch.from_numpy(lens.view(np.int32)).cuda(),
+                   out=out)
+    torch.cuda.synchronize()
+    want = O.crc32_ranges(t[:n].cpu().numpy(), offs, lens)
+    got = _u32(out)
+    assert np.array_equal(got, want), np.nonzero(got != want)[0][:8]
+    del t
+
+
 @pytest.mark.parametrize("register", [False, True])
 def test_ranges_host_scrub(torch_cuda, ctx, register):
     """Memfile-scrub form: extents of a host region read zero-copy over PCIe."""

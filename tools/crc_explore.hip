@@ -24,11 +24,6 @@
 namespace {
 #include "../priskv_amd/csrc/crc_device.inc"
 #include "crc_rows_explore.inc"
-#include "crc_dyn_explore.inc"
-#include "crc_pair_explore.inc"
-#include "crc_tail_explore.inc"
-#include "crc_rows2_explore.inc"
-#include "crc_steal_explore.inc"
 
 // read-only roof with the rows kernel's loop and addressing (same loads, no hashing)
 // TIMING: also write each wave's start / end s_memrealtime after the sink
@@ -229,6 +224,9 @@ struct Variant {
     std::vector<float> ms;
 };
 
+// nibble-table fold (OPT bit 5): the fold pointer is the nibble image
+static uint32_t *g_nib[65] = {};
+
 #define CRC_VARIANT_W(G, CH, NB, AUX, WGPC, OPT, WE, WO)                                                      \
     Variant{"crc G" #G " CH" #CH " NBUF" #NB " AUX" #AUX " wg/cu" #WGPC " opt" #OPT " xw" #WE ":" #WO, true, G, \
             CH, WGPC, OPT,                                                                                     \
@@ -266,53 +264,6 @@ struct Variant {
                 hipLaunchKernelGGL((roof_rows<G, CH, NB, AUX>), g, dim3(kThreads), 98304, s, b, n, bs, img, fold, \
                                    o, 0u);                                                                     \
             }, {}}
-#define CRC2_VARIANT(G, CH, NB, AUX, WGPC)                                                                     \
-    Variant{"crc2 G" #G " CH" #CH " NBUF" #NB " AUX" #AUX " wg/cu" #WGPC, true, G, CH, WGPC, -1,            \
-            [](dim3 g, hipStream_t s, const uint8_t *b, uint64_t n, uint32_t bs, const uint32_t *img,           \
-               const uint32_t *fold, uint32_t *o) {                                                            \
-                hipLaunchKernelGGL((crc_rows2_kernel<G, CH, NB, AUX>), g, dim3(kThreads), 0, s, b, n / 2, bs, img, \
-                                   fold, o);                                                                   \
-            }, {}}
-// dynamically balanced variants: tile size and ticket counter via globals
-static uint32_t *g_ctr = nullptr;
-#define DYN_VARIANT(G, CH, NB, AUX, WGPC, OPT)                                                                 \
-    Variant{((OPT) & 16 ? "roof dyn G" #G " CH" #CH " NBUF" #NB " wg/cu" #WGPC                                 \
-                        : "crc dyn G" #G " CH" #CH " NBUF" #NB " wg/cu" #WGPC " opt" #OPT),                     \
-            !((OPT) & 16), G, CH, WGPC, -1,                                                                    \
-            [](dim3 g, hipStream_t s, const uint8_t *b, uint64_t n, uint32_t bs, const uint32_t *img,           \
-               const uint32_t *fold, uint32_t *o) {                                                            \
-                (void)hipMemsetAsync(g_ctr, 0, 4, s);                                                          \
-                hipLaunchKernelGGL((crc_rows_dyn_kernel<G, CH, NB, AUX, OPT>), g, dim3(kThreads), 0, s, b, n, bs, \
-                                   img, fold, o, g_ctr);                                                       \
-            }, {}}
-// static head + per-XCD pooled tail (crc_tail_explore.inc): TS groups per
-// tile, K tiles per wave pooled; counters zeroed on the stream before each launch
-#define TAIL_VARIANT(G, CH, NB, AUX, OPT, WE, WO, TS, K)                                                       \
-    Variant{((OPT) & 16 ? "roof tail G" #G " CH" #CH " NBUF" #NB " ts" #TS " k" #K " xw" #WE ":" #WO          \
-                        : "crc tail G" #G " CH" #CH " NBUF" #NB " opt" #OPT " ts" #TS " k" #K " xw" #WE ":" #WO), \
-            !((OPT) & 16), G, CH, 1, -1,                                                                       \
-            [](dim3 g, hipStream_t s, const uint8_t *b, uint64_t n, uint32_t bs, const uint32_t *img,           \
-               const uint32_t *fold, uint32_t *o) {                                                            \
-                (void)hipMemsetAsync(g_ctr, 0, 4096, s);                                                       \
-                hipLaunchKernelGGL((crc_rows_tail_kernel<G, CH, NB, AUX, OPT>), g, dim3(kThreads), 0, s, b, n, bs, \
-                                   img, ((OPT) & 32) ? g_nib[G] : fold, o, (uint32_t)(((WE) << 16) | (WO)), g_ctr, \
-                                   (uint32_t)(TS), (uint32_t)(K));                                             \
-            }, {}}
-// paired (forward / backward wave pairs; NEGATIVE RESULT, explorer only --
-// profiles/r01/explore_4k_pair.log: per-XCD finish times equalize, but both
-// the CRC and the read roof lose 2-4 %): slots + epoch via globals
-static uint64_t *g_slots = nullptr;
-static uint32_t g_epoch = 0;
-#define PAIR_VARIANT(G, CH, NB, AUX, WGPC, OPT)                                                                \
-    Variant{((OPT) & 64 ? "roof pair G" #G " CH" #CH " NBUF" #NB " wg/cu" #WGPC " opt" #OPT                   \
-                        : "crc pair G" #G " CH" #CH " NBUF" #NB " wg/cu" #WGPC " opt" #OPT),                    \
-            !((OPT) & 64), G, CH, WGPC, (OPT) & 64 ? -1 : (OPT),                                               \
-            [](dim3 g, hipStream_t s, const uint8_t *b, uint64_t n, uint32_t bs, const uint32_t *img,           \
-               const uint32_t *fold, uint32_t *o) {                                                            \
-                g.x += g.x & 1;                                                                                \
-                hipLaunchKernelGGL((crc_rows_pair_kernel<G, CH, NB, AUX, OPT>), g, dim3(kThreads), 0, s, b, n, bs, \
-                                   img, fold, o, g_slots, ++g_epoch);                                          \
-            }, {}}
 #define ROOF_VARIANT_W(G, CH, NB, AUX, WGPC, WE, WO)                                                        \
     Variant{"roof G" #G " CH" #CH " NBUF" #NB " AUX" #AUX " wg/cu" #WGPC " xw" #WE ":" #WO, false, G, CH,     \
             WGPC, -1,                                                                                      \
@@ -339,21 +290,6 @@ static uint32_t g_epoch = 0;
                const uint32_t *fold, uint32_t *o) {                                                        \
                 hipLaunchKernelGGL((roof_rows<G, CH, NB, AUX, true>), g, dim3(kThreads), 0, s, b, n, bs, img, fold, \
                                    o, (uint32_t)(((WE) << 16) | (WO)));                                    \
-            }, {}}
-// nibble-table fold (OPT bit 5): the fold pointer is the nibble image
-static uint32_t *g_nib[65] = {};
-// work stealing (crc_steal_explore.inc): claim words + a 4-bit launch epoch
-static uint64_t *g_claims = nullptr;
-static uint32_t g_epoch_s = 0;
-#define STEAL_VARIANT(G, CH, NB, AUX, OPT, WE, WO, T16, U)                                                     \
-    Variant{"steal G" #G " CH" #CH " NBUF" #NB " opt" #OPT " xw" #WE ":" #WO " t" #T16 " u" #U, true, G, CH, 1, \
-            (OPT),                                                                                             \
-            [](dim3 g, hipStream_t s, const uint8_t *b, uint64_t n, uint32_t bs, const uint32_t *img,           \
-               const uint32_t *fold, uint32_t *o) {                                                            \
-                g_epoch_s = (g_epoch_s + 1) & 15u;                                                             \
-                hipLaunchKernelGGL((crc_rows_steal_kernel<G, CH, NB, AUX, OPT>), g, dim3(kThreads), 0, s, b, n, bs, \
-                                   img, ((OPT) & 32) ? g_nib[G] : fold, o, (uint32_t)(((WE) << 16) | (WO)),     \
-                                   g_claims, (g_epoch_s << 28) | ((uint32_t)(T16) << 16) | (uint32_t)(U));      \
             }, {}}
 // slice-by-8 pairs (OPT bit 6): 128 KiB image [Z_4 sets | Z_8 sets]
 static uint32_t *g_img8[65] = {};
@@ -519,11 +455,6 @@ int main(int argc, char **argv)
                        0ull);
     CK(hipDeviceSynchronize());
 
-    CK(hipMalloc(&g_ctr, 4096));
-    CK(hipMalloc(&g_slots, (size_t)ncu * 2 * kWaves * 128));
-    CK(hipMemset(g_slots, 0, (size_t)ncu * 2 * kWaves * 128));
-    CK(hipMalloc(&g_claims, (size_t)ncu * 16 * 8));
-    CK(hipMemset(g_claims, 0, (size_t)ncu * 16 * 8));
     std::vector<Variant> all;
     // first entry = product reference for the bit-exact cross-check and the sustained run
     all.push_back(CRC_VARIANT_W(32, 8, 2, 2, 1, 2, 31, 29));
@@ -595,18 +526,6 @@ int main(int argc, char **argv)
     all.push_back(ROOFC_VARIANT(32, 8, 2, 2, 8));
     all.push_back(ROOFC_VARIANT(32, 8, 2, 2, 32));
     all.push_back(ROOFC_VARIANT(32, 8, 2, 2, 128));
-    all.push_back(STEAL_VARIANT(32, 8, 2, 2, 2 | 32 | 768, 31, 29, 4, 8));
-    all.push_back(STEAL_VARIANT(32, 8, 2, 2, 2 | 32 | 768, 31, 29, 4, 16));
-    all.push_back(STEAL_VARIANT(32, 8, 2, 2, 2 | 32 | 768, 31, 29, 2, 8));
-    all.push_back(STEAL_VARIANT(32, 8, 2, 2, 2 | 32 | 768, 31, 29, 8, 8));
-    all.push_back(STEAL_VARIANT(32, 8, 2, 2, 2 | 32 | 768, 31, 29, 4, 4));
-    all.push_back(STEAL_VARIANT(32, 8, 2, 2, 2 | 32 | 768, 0, 0, 4, 8));
-    all.push_back(STEAL_VARIANT(32, 8, 2, 2, 2 | 32 | 768, 31, 29, 16, 8));
-    all.push_back(STEAL_VARIANT(32, 8, 2, 2, 2 | 32 | 768 | 8, 31, 29, 4, 8));
-    all.push_back(STEAL_VARIANT(64, 4, 2, 2, 256, 31, 29, 4, 1));
-    all.push_back(STEAL_VARIANT(64, 4, 2, 2, 256, 31, 29, 2, 1));
-    all.push_back(STEAL_VARIANT(64, 4, 2, 2, 256, 31, 29, 4, 2));
-    all.push_back(STEAL_VARIANT(64, 4, 2, 2, 256 | 8, 31, 29, 4, 1));
     all.push_back(CRC_VARIANT_W(64, 4, 2, 2, 1, 256 | 8, 31, 29));
     all.push_back(S8_VARIANT_W(32, 8, 2, 2, 1, 2, 31, 29));
     all.push_back(NIB_VARIANT_W(32, 8, 2, 2, 1, 2, 0, 0));
@@ -668,14 +587,6 @@ int main(int argc, char **argv)
     all.push_back(ROOF_VARIANT_W(32, 8, 2, 0, 1, 31, 29));
     all.push_back(ROOF_VARIANT_W(32, 8, 2, 3, 1, 31, 29));
     all.push_back(ROOF_VARIANT_W(32, 8, 2, 18, 1, 31, 29));
-    all.push_back(TAIL_VARIANT(32, 8, 2, 2, 34, 31, 29, 8, 4));
-    all.push_back(TAIL_VARIANT(32, 8, 2, 2, 34, 31, 29, 4, 8));
-    all.push_back(TAIL_VARIANT(32, 8, 2, 2, 34, 31, 29, 16, 4));
-    all.push_back(TAIL_VARIANT(32, 8, 2, 2, 34, 31, 29, 8, 8));
-    all.push_back(TAIL_VARIANT(32, 8, 2, 2, 34, 0, 0, 8, 4));
-    all.push_back(TAIL_VARIANT(32, 8, 2, 2, 34, 0, 0, 8, 8));
-    all.push_back(TAIL_VARIANT(32, 8, 2, 2, 16, 31, 29, 8, 4));
-    all.push_back(TAIL_VARIANT(64, 4, 2, 2, 0, 31, 29, 4, 4));
     all.push_back(ROOF_T_VARIANT(32, 8, 2, 2, 1, 31, 29));
     all.push_back(ROOF_T_VARIANT(32, 8, 2, 2, 1, 0, 0));
     all.push_back(NIB_VARIANT_W(32, 8, 2, 2, 1, 10, 31, 29));
@@ -700,15 +611,6 @@ int main(int argc, char **argv)
     all.push_back(CRC_VARIANT_W(32, 8, 2, 2, 1, 6, 31, 29));
     all.push_back(ROOF_VARIANT_W(32, 8, 3, 2, 1, 31, 29));
     all.push_back(ROOF_VARIANT_W(32, 8, 2, 2, 1, 31, 29));
-    all.push_back(PAIR_VARIANT(32, 8, 2, 2, 1, 2));
-    all.push_back(PAIR_VARIANT(32, 8, 2, 2, 1, 10));
-    all.push_back(PAIR_VARIANT(32, 8, 2, 2, 1, 66));
-    all.push_back(PAIR_VARIANT(32, 8, 2, 2, 1, 194));
-    all.push_back(PAIR_VARIANT(32, 8, 2, 2, 1, 322));
-    all.push_back(PAIR_VARIANT(32, 8, 2, 2, 1, 258));
-    all.push_back(PAIR_VARIANT(64, 4, 2, 2, 1, 0));
-    all.push_back(PAIR_VARIANT(64, 4, 2, 2, 1, 8));
-    all.push_back(PAIR_VARIANT(64, 4, 2, 2, 1, 64));
     all.push_back(CRC_VARIANT_W(32, 8, 2, 2, 1, 2, 41, 39));
     all.push_back(CRC_VARIANT_OS(32, 8, 2, 2, 2, 2, 0, 0));
     all.push_back(CRC_VARIANT_OS(32, 8, 2, 2, 2, 2, 31, 29));

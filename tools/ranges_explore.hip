@@ -25,7 +25,6 @@
 
 namespace {
 #include "../priskv_amd/csrc/crc_device.inc"
-#include "crc_ranges2_explore.inc"
 } // namespace
 
 #define CK(x)                                                                                      \
@@ -54,13 +53,6 @@ struct Variant {
                 hipLaunchKernelGGL((crc_ranges_kernel<CH, NB, AUX>), g, dim3(kThreads), 0, 0, b, n, o, l, 0ull,   \
                                    stride, lc, img, fold, un, out, nullptr, nullptr, nullptr, nullptr);                              \
             }, false}
-#define RV2(CH, NB, AUX, WG)                                                                                   \
-    Variant{"ext2 CH" #CH " NBUF" #NB " AUX" #AUX " wg/cu" #WG, WG,                                            \
-            [](dim3 g, const uint8_t *b, uint64_t n, const uint64_t *o, const uint32_t *l, uint64_t stride,       \
-               uint32_t lc, const uint32_t *img, const uint32_t *fold, const uint32_t *un, uint32_t *out) {       \
-                hipLaunchKernelGGL((crc_ranges2_kernel<CH, NB, AUX>), g, dim3(kThreads), 0, 0, b, n, o, l, 0ull,  \
-                                   stride, lc, img, fold, un, out, nullptr, nullptr, nullptr, nullptr);                              \
-            }, true}
 
 // OPT bit 0 (nibble fold) takes its two images from these globals
 static uint32_t *g_nib16 = nullptr, *g_rowshift = nullptr;
@@ -81,6 +73,17 @@ static uint32_t *g_nib16 = nullptr, *g_rowshift = nullptr;
                 hipLaunchKernelGGL((crc_ranges_kernel<CH, NB, AUX, (OPT) | 1024>), g, dim3(1024), 0, 0, b, n, o, l, \
                                    0ull, stride, lc, img, ((OPT) & 1) ? g_nib16 : fold,                           \
                                    ((OPT) & 1) ? g_rowshift : un, out, nullptr, nullptr, nullptr, nullptr);       \
+            }, false}
+
+// 16-wave workgroups, WG of them per CU (OPT without progress priority fits
+// two 80 KiB workgroups in the CU's 160 KiB of LDS)
+#define RVO16W(CH, NB, AUX, OPT, WG)                                                                          \
+    Variant{"ext CH" #CH " NBUF" #NB " AUX" #AUX " 16 waves x" #WG " opt" #OPT, WG,                             \
+            [](dim3 g, const uint8_t *b, uint64_t n, const uint64_t *o, const uint32_t *l, uint64_t stride,       \
+               uint32_t lc, const uint32_t *img, const uint32_t *fold, const uint32_t *un, uint32_t *out) {       \
+                hipLaunchKernelGGL((crc_ranges_kernel<CH, NB, AUX, (OPT) | 1024>), g, dim3(1024), 0, 0, b, n, o, l, \
+                                   0ull, stride, lc, img, g_nib16, g_rowshift, out, nullptr, nullptr, nullptr,     \
+                                   nullptr);                                                                      \
             }, false}
 
 struct Set {
@@ -154,6 +157,20 @@ int main(int argc, char **argv)
         sets.push_back(s);
     };
     add("priskv", off, len);
+    if (getenv("RANGES_SPANS")) { // PrisKV-shaped values of one span each: 1, 2, 4 blocks
+        for (int sp = 0; sp < 3; sp++) {
+            std::vector<uint64_t> o1(n);
+            std::vector<uint32_t> l1(n);
+            for (uint64_t i = 0; i < n; i++) {
+                const uint64_t span = (1ull << sp) * bs;
+                const uint64_t blk = rng() % (region / bs - 4);
+                o1[i] = blk * bs;
+                l1[i] = (uint32_t)std::min<uint64_t>(span - rng() % bs, region - o1[i]);
+            }
+            static const char *nm[3] = {"span1", "span2", "span4"};
+            add(nm[sp], o1, l1);
+        }
+    }
     {
         std::vector<uint64_t> idx(n);
         std::iota(idx.begin(), idx.end(), 0);
@@ -183,6 +200,20 @@ int main(int argc, char **argv)
 
     std::vector<Variant> V = {RVO(2, 2, 2, 2, 3),         RVO16(2, 2, 2, 3),       RVO16(2, 2, 2, 3 | 256),
                               RVO16(2, 2, 2, 3 | 512),    RVO16(2, 2, 2, 3 | 768)};
+    if (getenv("RANGES_R3")) // round 3: product, skipped virtual rows (8192), read roof (4096), shapes
+        V = {RVO16(2, 2, 2, 3 | 768),        RVO16(2, 2, 2, 3 | 768 | 8192), RVO16(2, 2, 2, 3 | 768 | 4096),
+             RVO16(2, 3, 2, 3 | 768 | 8192), RVO16(4, 2, 2, 3 | 768 | 8192), RVO16(1, 4, 2, 3 | 768 | 8192),
+             RVO16(2, 3, 2, 3 | 768 | 4096), RVO16(4, 2, 2, 3 | 768 | 4096), RVO16W(2, 2, 2, 3 | 8192, 2),
+             RVO16W(2, 3, 2, 3 | 8192, 2), RVO16W(2, 2, 2, 3 | 4096, 2)};
+    if (getenv("RANGES_R3B")) // round 3: chunk shapes of the many-extents launch shape
+        V = {RVO16(2, 2, 2, 3 | 768),        RVO16(4, 2, 2, 3 | 768),        RVO16(4, 3, 2, 3 | 768),
+             RVO16(8, 2, 2, 3 | 768),        RVO16(4, 2, 2, 3 | 256),        RVO16(4, 2, 2, 3),
+             RVO16(4, 3, 2, 3 | 768 | 4096), RVO16(8, 2, 2, 3 | 768 | 4096)};
+    if (getenv("RANGES_R3C")) // round 3: CH2 against CH4 / CH8 by value span
+        V = {RVO16(2, 2, 2, 3 | 768), RVO16(4, 2, 2, 3 | 768), RVO16(8, 2, 2, 3 | 768)};
+    if (getenv("RANGES_R3D")) // round 3: the per-wave chunk size (OPT bit 14) against fixed CH2 / CH4 / CH8
+        V = {RVO16(2, 2, 2, 3 | 768), RVO16(2, 2, 2, 3 | 768 | 16384), RVO16(4, 2, 2, 3 | 768),
+             RVO16(8, 2, 2, 3 | 768)};
     if (getenv("RANGES_ALL")) // the earlier CH / NBUF / fold sweep
         V = {RV(2, 2, 2, 2),     RVO(2, 2, 2, 2, 1), RVO(2, 2, 2, 2, 2), RVO(2, 2, 2, 2, 3),
              RVO(1, 4, 2, 2, 3), RVO(2, 3, 2, 2, 3), RVO(4, 2, 2, 2, 3)};
@@ -225,7 +256,7 @@ int main(int argc, char **argv)
                         std::vector<uint32_t> a(s.n), b(s.n);
                         CK(hipMemcpy(a.data(), d_ref, s.n * 4, hipMemcpyDeviceToHost));
                         CK(hipMemcpy(b.data(), d_out, s.n * 4, hipMemcpyDeviceToHost));
-                        if (memcmp(a.data(), b.data(), s.n * 4)) {
+                        if (!strstr(V[vi].name, "4096") && memcmp(a.data(), b.data(), s.n * 4)) { // 4096: roof
                             printf("MISMATCH %s %s\n", s.name, V[vi].name);
                             ok_all = false;
                         }
