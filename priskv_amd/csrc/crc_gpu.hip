@@ -72,6 +72,7 @@ struct priskv_crc_ctx {
     int prio;                  // rows kernel progress priority (PRISKV_CRC_PRIO=0: off)
     int balance;               // byte-balanced extents split (PRISKV_CRC_BALANCE=0: off)
     int ext_adapt;             // per-wave chunk size of the many-extents shape (PRISKV_CRC_EXT_ADAPT=0: 2 rows)
+    int fused_ch;              // rows per chunk of the fused few-extents kernel (PRISKV_CRC_FUSED_CH=2/4/8; tuning)
     uint64_t seg_max_extents;  // device-resident lengths: segment calls of at most this many extents
     int xcd_rr;                // the XCD probe found workgroup b on XCD b % 8 (weights apply)
     uint64_t tile_min_bytes;   // rows batches of at least this many bytes run in block-cyclic tiles
@@ -577,6 +578,7 @@ constexpr uint32_t kSegMinLen = 64u << 10;
 // progress priority off in the fused kernel: 1 x 256 MiB 49.7 us vs 50.7 with
 // mode 3, 4096 small values 7.6 vs 7.7 us (profiles/r02/fused/ktrace_shapes_*)
 constexpr int kFusedPrio = 0;
+constexpr int kFusedCh = 2; // rows per chunk (PRISKV_CRC_FUSED_CH)
 
 // one segment size per call (crc_seg_plan_kernel / the fused kernel): about
 // kSegPerWave full segments per resident wave, so the count split of
@@ -617,11 +619,18 @@ int launch_fused(const priskv_crc_ctx *ctx, const uint8_t *base, uint64_t n, con
     const uint8_t *abase = base - sh;
     const uint32_t *lens_or_null = offs ? lens : nullptr;
     const uint32_t tgt = 1u << (31 - __builtin_clz((uint32_t)seg_target(ctx))); // the kernel takes a power of two
-    hipLaunchKernelGGL((crc_ranges_fused_kernel<kExtRows, kNbuf, kAux, kFusedPrio, kFusedWaves>), dim3(grid),
-                       dim3(64 * kFusedWaves), 0, s, abase, n, offs, lens_or_null, sh, stride, len_const,
-                       ctx->d_lds_image[0], ctx->d_nib16, ctx->d_rowshift, out, ctx->d_zpow, tgt, kSegMinShift, cnt,
-                       xacc);
-    const int rc = herr(hipGetLastError());
+    const void *fn = ctx->fused_ch == 8 ? reinterpret_cast<const void *>(
+                                              &crc_ranges_fused_kernel<8, kNbuf, kAux, kFusedPrio, kFusedWaves>)
+                     : ctx->fused_ch == 4 ? reinterpret_cast<const void *>(
+                                              &crc_ranges_fused_kernel<4, kNbuf, kAux, kFusedPrio, kFusedWaves>)
+                                          : reinterpret_cast<const void *>(
+                                              &crc_ranges_fused_kernel<kExtRows, kNbuf, kAux, kFusedPrio, kFusedWaves>);
+    const uint32_t *img = ctx->d_lds_image[0], *nib = ctx->d_nib16, *rs = ctx->d_rowshift, *zp = ctx->d_zpow;
+    uint32_t ms = kSegMinShift;
+    void *args[] = {(void *)&abase, (void *)&n,   (void *)&offs, (void *)&lens_or_null, (void *)&sh,
+                    (void *)&stride, (void *)&len_const, (void *)&img, (void *)&nib, (void *)&rs,
+                    (void *)&out,   (void *)&zp,  (void *)&tgt, (void *)&ms, (void *)&cnt, (void *)&xacc};
+    const int rc = herr(hipLaunchKernel(fn, dim3(grid), dim3(64 * kFusedWaves), args, 0, s));
     const int frc = sc.release();
     return rc ? rc : frc;
 }
@@ -1120,6 +1129,10 @@ int priskv_crc_ctx_create(int device, priskv_crc_ctx **out)
         c->balance = !(be && !strcmp(be, "0"));
         const char *ea = getenv("PRISKV_CRC_EXT_ADAPT");
         c->ext_adapt = !(ea && !strcmp(ea, "0"));
+        const char *fc = getenv("PRISKV_CRC_FUSED_CH");
+        c->fused_ch = fc ? atoi(fc) : kFusedCh;
+        if (c->fused_ch != 2 && c->fused_ch != 4 && c->fused_ch != 8)
+            c->fused_ch = kFusedCh;
         const char *fe = getenv("PRISKV_CRC_FUSED");
         c->fused = !(fe && !strcmp(fe, "0"));
         const char *se = getenv("PRISKV_CRC_STRIDE");

@@ -157,6 +157,18 @@ int main(int argc, char **argv)
         sets.push_back(s);
     };
     add("priskv", off, len);
+    if (getenv("RANGES_PK64K")) { // PrisKV-shaped values on 64 KiB blocks (few per wave)
+        const uint64_t n64 = 1 << 15, bs64 = 65536;
+        std::vector<uint64_t> o1(n64);
+        std::vector<uint32_t> l1(n64);
+        for (uint64_t i = 0; i < n64; i++) {
+            const uint64_t span = (1ull << (rng() % 3)) * bs64;
+            const uint64_t blk = rng() % (region / bs64 - 4);
+            o1[i] = blk * bs64;
+            l1[i] = (uint32_t)std::min<uint64_t>(span - rng() % bs64, region - o1[i]);
+        }
+        add("pk64k", o1, l1);
+    }
     if (getenv("RANGES_SPANS")) { // PrisKV-shaped values of one span each: 1, 2, 4 blocks
         for (int sp = 0; sp < 3; sp++) {
             std::vector<uint64_t> o1(n);
@@ -214,6 +226,8 @@ int main(int argc, char **argv)
     if (getenv("RANGES_R3D")) // round 3: the per-wave chunk size (OPT bit 14) against fixed CH2 / CH4 / CH8
         V = {RVO16(2, 2, 2, 3 | 768), RVO16(2, 2, 2, 3 | 768 | 16384), RVO16(4, 2, 2, 3 | 768),
              RVO16(8, 2, 2, 3 | 768)};
+    if (getenv("RANGES_R3E")) // round 3: the per-wave chunk size in the two 8-wave workgroups shape
+        V = {RVO(2, 2, 2, 2, 3), RVO(2, 2, 2, 2, 3 | 16384), RVO(4, 2, 2, 2, 3), RVO(8, 2, 2, 2, 3)};
     if (getenv("RANGES_ALL")) // the earlier CH / NBUF / fold sweep
         V = {RV(2, 2, 2, 2),     RVO(2, 2, 2, 2, 1), RVO(2, 2, 2, 2, 2), RVO(2, 2, 2, 2, 3),
              RVO(1, 4, 2, 2, 3), RVO(2, 3, 2, 2, 3), RVO(4, 2, 2, 2, 3)};
