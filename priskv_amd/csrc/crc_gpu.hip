@@ -295,7 +295,7 @@ constexpr int kNbuf = 2;  // register pipeline depth (chunks) of the extents ker
 constexpr int kAux = 2;   // cache policy of the streaming loads: nt
 constexpr int kExtRows = 2; // rows per chunk of the extents kernel (tools/ranges_explore)
 // extents kernel: nibble fold + row apply (bit 0), masks only where needed
-// (bit 1).  Two shapes (profiles/r01/prio/): two 8-wave workgroups per CU
+// (bit 1).  Two shapes (profiles/r01/prio/ranges_prio_16w_*.log): two 8-wave workgroups per CU
 // (kExtOpt), and for calls with many extents per wave one 16-wave workgroup
 // per CU with progress-priority mode 3 (kExtOptMany: bits 8-9 and 10; the
 // progress slots do not fit beside two 80 KiB table sets in 160 KiB of LDS).
@@ -471,7 +471,7 @@ const void *plan_fn(int p, bool prio)
 
 // Block-cyclic tiles for big batches (crc_rows_kernel `tile`): groups per
 // tile, 0 = the contiguous per-wave split.  64 KiB blocks, 1 MiB tiles
-// against contiguous ranges, same box (profiles/r02/tiles/lib_*.json,
+// against contiguous ranges, same box (profiles/r02/tiles/lib_runs.jsonl,
 // tools/lib_timing): 16 GiB 2.558 / 2.436 ms, 32 GiB 4.888 / 4.874,
 // 64 GiB 9.859 / 9.802, 128 GiB 20.04 / 21.38 (+6.7 % for tiles; +5.7 % in
 // the explorer on another box, explore_r2r_*).  On some boxes the contiguous
