@@ -11,8 +11,9 @@ after a warm ramp, every context interleaved round by round in one process
   one256m    one 256 MiB value (the fused few-extents kernel)
   blk256m    one 256 MiB block through blocks_dev (fused kernel, one length)
 
-usage: values_bench.py [ROUNDS] [ENV=VALUE ...]   (each ENV=VALUE adds a
-context created with that variable set, beside the default one)
+usage: values_bench.py [ROUNDS] [ENV=VALUE[:ENV=VALUE...] ...]   (each
+argument adds a context created with those variables set, beside the
+default one)
 One JSON line per (case, context) with the median over rounds; every
 context's CRCs are compared with the default context's and, on a sample,
 with the CPU oracle.
@@ -49,11 +50,13 @@ def main():
     rounds = int(sys.argv[1]) if len(sys.argv) > 1 and sys.argv[1].isdigit() else 7
     ctxs = [("default", CrcContext(0))]
     for a in sys.argv[1:]:
-        if "=" in a:
-            k, v = a.split("=", 1)
-            os.environ[k] = v
+        if "=" in a:  # VAR=VALUE[:VAR=VALUE...]: one context with all of them set
+            kv = [x.split("=", 1) for x in a.split(":")]
+            for k, v in kv:
+                os.environ[k] = v
             ctxs.append((a, CrcContext(0)))
-            del os.environ[k]
+            for k, _ in kv:
+                del os.environ[k]
     region = 4 << 30
     t = torch.empty(region, dtype=torch.uint8, device="cuda")
     ctxs[0][1].fill_splitmix(t, 0x5EED5EED, 0)
