@@ -213,7 +213,11 @@ class Bench:
 
     def timed(self, step, stream, k):
         """k back-to-back steps between barrier + synchronize on both sides:
-        (max-over-ranks wall seconds, this rank's kernel ms per step)."""
+        (max-over-ranks wall seconds, this rank's kernel ms per step).  Every
+        rank starts its clock as the opening barrier releases it and stops
+        it once its own device has drained; the max over ranks is the job's
+        time, and the closing barrier's own latency (a collective, not the
+        path) stays outside it."""
         torch = self.torch
         ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         self.barrier()
@@ -224,8 +228,8 @@ class Bench:
             step()
         ev1.record(stream)
         torch.cuda.synchronize()
-        self.barrier()
         el = time.perf_counter() - t0
+        self.barrier()
         return self.max(el), ev0.elapsed_time(ev1) / k
 
     def alloc(self, nbytes):
@@ -522,18 +526,32 @@ def main():
     del out
     torch.cuda.empty_cache()
 
+    def leg(fn, *a, **kw):
+        """A leg beside the headline.  On one rank a failure is reported in
+        the line instead of losing the headline; with several ranks it
+        propagates (its collectives could no longer pair up)."""
+        if world > 1:
+            return fn(*a, **kw)
+        try:
+            return fn(*a, **kw)
+        except Exception as e:  # noqa: BLE001 -- reported in the line
+            torch.cuda.synchronize()
+            torch.cuda.empty_cache()
+            return {"error": f"{type(e).__name__}: {e}"}
+
     if not args.no_sweep and args.config == "default":
-        result["sweep"] = {k: resident_leg(B, name, args.sweep_steps) for k, name in SWEEP}
+        result["sweep"] = {k: leg(resident_leg, B, name, args.sweep_steps) for k, name in SWEEP}
     if not args.no_tib and args.config == "default":
-        result["tib"] = resident_leg(B, "tib", args.tib_steps, parity="sampled")
+        result["tib"] = leg(resident_leg, B, "tib", args.tib_steps, parity="sampled")
     if not args.no_streamed:
-        result["streamed"] = streamed_leg(B, host, bs, want)
+        result["streamed"] = leg(streamed_leg, B, host, bs, want)
     # cold passes LAST on the GPU: what a one-off recovery scrub sees (clock
     # ramp included); measured last so that the idle cannot leave its slower
     # first launches inside the other legs
     if walked is not None:
-        result["cold"] = cold_leg(B, bs, nb, walked)
-        result["cold_ms"] = result["cold"]["ms"]
+        result["cold"] = leg(cold_leg, B, bs, nb, walked)
+        if "ms" in result["cold"]:
+            result["cold_ms"] = result["cold"]["ms"]
         del walked
     torch.cuda.empty_cache()
 
