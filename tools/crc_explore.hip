@@ -96,6 +96,73 @@ __global__ __launch_bounds__(kThreads, rows_min_wg(CH, NBUF)) void roof_rows(con
     }
 }
 
+// read-only roof, workgroup-interleaved: each workgroup owns a contiguous
+// range of groups (split by workgroup, even:odd XCD weights xw) and wave w
+// of it reads groups w, w + 8, w + 16, ... of that range, so the chip reads
+// 256 streams of 8 adjacent groups instead of 2048 per-wave streams
+// (tools/xcd_locality_probe: 8 waves interleaved read 1.8 % faster)
+template <int G, int CH, int NBUF, int AUX>
+__global__ __launch_bounds__(kThreads, rows_min_wg(CH, NBUF)) void roof_wgil(const uint8_t *__restrict__ base,
+                                                                            uint64_t ngroups, uint32_t block_size,
+                                                                            const uint32_t *, const uint32_t *,
+                                                                            uint32_t *__restrict__ out, uint32_t xw)
+{
+    constexpr int NB = 64 / G, RB = 16 * G;
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    uint64_t G0, NG;
+    wave_range<1>(ngroups, gridDim.x, blockIdx.x, xw, G0, NG);
+    const uint64_t ng = NG > (uint64_t)wave ? (NG - wave + kWaves - 1) / kWaves : 0;
+    if (ng == 0)
+        return;
+    const uint32_t cps = block_size / (CH * RB);
+    const uint32_t nq = __builtin_amdgcn_readfirstlane((uint32_t)ng * cps);
+    const uint32_t span = (NB - 1) * block_size + CH * RB;
+    const uint32_t voff = (uint32_t)(lane / G) * block_size + (uint32_t)(lane % G) * 16;
+    const uint64_t gstride = (uint64_t)NB * block_size;
+    const uint32_t cstride = CH * RB;
+    const uint8_t *pp = base + (G0 + wave) * gstride;
+    uint32_t pc = 0, pq = 0;
+    auto advance = [&]() {
+        if (pq + 1 < nq) {
+            pq++;
+            if (++pc == cps) {
+                pc = 0;
+                pp += kWaves * gstride - (uint64_t)(cps - 1) * cstride;
+            } else {
+                pp += cstride;
+            }
+        }
+    };
+    v4u buf[NBUF][CH];
+#pragma unroll
+    for (int j = 0; j < NBUF - 1; j++) {
+        load_chunk<CH, RB, AUX>(buf[j], pp, span, voff);
+        advance();
+    }
+    uint32_t acc = 0, q = 0;
+    for (; q + NBUF <= nq; q += NBUF) {
+#pragma unroll
+        for (int j = 0; j < NBUF; j++) {
+            load_chunk<CH, RB, AUX>(buf[(j + NBUF - 1) % NBUF], pp, span, voff);
+            advance();
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int k = 0; k < CH; k++)
+                acc ^= buf[j][k].x ^ buf[j][k].y ^ buf[j][k].z ^ buf[j][k].w;
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < NBUF - 1; j++) {
+        if (q + j >= nq)
+            break;
+#pragma unroll
+        for (int k = 0; k < CH; k++)
+            acc ^= buf[j][k].x ^ buf[j][k].y ^ buf[j][k].z ^ buf[j][k].w;
+    }
+    out[((uint64_t)blockIdx.x * kWaves + wave) * 64 + lane] = acc;
+}
+
 // read-only roof, block-cyclic: wave w reads tiles w, w + W, w + 2W, ...
 // of TILE groups each (contiguous inside a tile), so at any moment the chip
 // touches a window of about W * TILE groups instead of W ranges spread over
@@ -273,6 +340,14 @@ static uint32_t *g_nib[65] = {};
                                    (uint32_t)(((WE) << 16) | (WO)));                                       \
             }, {}}
 #define ROOF_VARIANT(G, CH, NB, AUX, WGPC) ROOF_VARIANT_W(G, CH, NB, AUX, WGPC, 0, 0)
+#define ROOFIL_VARIANT_W(G, CH, NB, AUX, WGPC, WE, WO)                                                      \
+    Variant{"roofwgil G" #G " CH" #CH " NBUF" #NB " AUX" #AUX " wg/cu" #WGPC " xw" #WE ":" #WO, false, G, CH, \
+            WGPC, -1,                                                                                      \
+            [](dim3 g, hipStream_t s, const uint8_t *b, uint64_t n, uint32_t bs, const uint32_t *img,       \
+               const uint32_t *fold, uint32_t *o) {                                                        \
+                hipLaunchKernelGGL((roof_wgil<G, CH, NB, AUX>), g, dim3(kThreads), 0, s, b, n, bs, img, fold, o, \
+                                   (uint32_t)(((WE) << 16) | (WO)));                                       \
+            }, {}}
 #define ROOFC_VARIANT(G, CH, NB, AUX, TILE)                                                                 \
     Variant{"roofcyc G" #G " CH" #CH " NBUF" #NB " AUX" #AUX " tile" #TILE, false, G, CH, 1, -1,           \
             [](dim3 g, hipStream_t s, const uint8_t *b, uint64_t n, uint32_t bs, const uint32_t *img,       \
@@ -662,6 +737,16 @@ int main(int argc, char **argv)
     all.push_back(ROOF_VARIANT_W(64, 4, 3, 2, 2, 31, 29));
     all.push_back(ROOF_VARIANT_W(64, 4, 2, 2, 3, 31, 29));
     all.push_back(ROOF_VARIANT_W(64, 2, 4, 2, 1, 31, 29));
+    // round 3: workgroup-interleaved streams against per-wave streams
+    all.push_back(PROD_VARIANT(64, 4, 2, 2 | 32 | 768, 31, 29));
+    all.push_back(ROOFIL_VARIANT_W(64, 4, 3, 2, 1, 31, 29));
+    all.push_back(ROOFIL_VARIANT_W(64, 4, 3, 2, 1, 0, 0));
+    all.push_back(ROOFIL_VARIANT_W(64, 4, 2, 2, 1, 31, 29));
+    all.push_back(ROOFIL_VARIANT_W(64, 4, 2, 2, 1, 0, 0));
+    all.push_back(ROOFIL_VARIANT_W(64, 4, 4, 2, 1, 31, 29));
+    all.push_back(ROOFIL_VARIANT_W(64, 2, 4, 2, 1, 31, 29));
+    all.push_back(ROOFIL_VARIANT_W(64, 2, 2, 2, 1, 31, 29));
+    all.push_back(ROOF_VARIANT_W(64, 4, 2, 2, 1, 31, 29));
     // EXPLORE_FILTER="a,b,c": keep only variants whose name contains one of the substrings
     std::vector<std::string> filt;
     if (const char *f = getenv("EXPLORE_FILTER")) {
