@@ -184,7 +184,9 @@ int priskv_crc_fill_splitmix_dev(const priskv_crc_ctx *ctx, void *d_dst, uint64_
  * 16 B up to 4.5 KiB when the size or base is not a multiple of 4, up to
  * 9 KiB otherwise: rows aligned to each block's end), 2 = extents (the
  * larger such blocks, and every block beyond 64 MiB), 4 = generic (blocks
- * below 16 B: one thread per block).  Context options (PRISKV_CRC_STRIDE=0,
+ * below 16 B: one thread per block), 6 = head split (a multiple of 4 that is
+ * whole KiB rows plus a 4-64 B head, 4-byte aligned base: the rows kernel on
+ * the bodies, then the heads' terms).  Context options (PRISKV_CRC_STRIDE=0,
  * PRISKV_CRC_STRIDE_MAX_KIB) move the 5 / 2 boundary; the exact kernels a
  * given context launches, few-block segmentation included, are reported by
  * priskv_crc32_blocks_plan.  For tests and benchmarks; -EINVAL for invalid

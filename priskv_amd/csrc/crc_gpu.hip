@@ -72,6 +72,7 @@ struct priskv_crc_ctx {
     int prio;                  // rows kernel progress priority (PRISKV_CRC_PRIO=0: off)
     int balance;               // byte-balanced extents split (PRISKV_CRC_BALANCE=0: off)
     int ext_adapt;             // per-wave chunk size of the many-extents shape (PRISKV_CRC_EXT_ADAPT=0: 2 rows)
+    int head_split;            // rows kernel + head terms for B = h + whole KiB rows (PRISKV_CRC_HEADSPLIT=0: off)
     int fused_ch;              // rows per chunk of the fused few-extents kernel (PRISKV_CRC_FUSED_CH=2/4/8; tuning)
     uint64_t seg_max_extents;  // device-resident lengths: segment calls of at most this many extents
     int xcd_rr;                // the XCD probe found workgroup b on XCD b % 8 (weights apply)
@@ -252,7 +253,7 @@ struct Scratch {
 
 inline bool is_pow2(uint64_t v) { return v && !(v & (v - 1)); }
 
-enum Path { PATH_ROWS = 1, PATH_EXTENTS = 2, PATH_SMALL = 3, PATH_GENERIC = 4, PATH_STRIDE = 5 };
+enum Path { PATH_ROWS = 1, PATH_EXTENTS = 2, PATH_SMALL = 3, PATH_GENERIC = 4, PATH_STRIDE = 5, PATH_HEAD = 6 };
 
 // stride = 0: round 2's dispatch of odd sizes / unaligned bases (extents from
 // 1 KiB, generic below)
@@ -489,9 +490,12 @@ uint32_t tile_groups(const priskv_crc_ctx *ctx, uint64_t ngroups, uint64_t gstri
     return t ? (uint32_t)(t < (1u << 20) ? t : (1u << 20)) : 1u;
 }
 
+// stride: bytes from block to block (0: bs; more for the head-split bodies)
 int launch_plan(const priskv_crc_ctx *ctx, int p, const uint8_t *base, uint64_t ngroups, uint32_t bs, uint32_t *out,
-                hipStream_t s)
+                hipStream_t s, uint32_t stride = 0)
 {
+    if (!stride)
+        stride = bs;
     const Plan &P = kPlans[p];
     const int gi = P.G == 64 ? 0 : (P.G == 32 ? 1 : 2);
     const uint64_t max_wgs = (uint64_t)ctx->num_cus * ctx->plan_wgs_per_cu[p];
@@ -503,15 +507,15 @@ int launch_plan(const priskv_crc_ctx *ctx, int p, const uint8_t *base, uint64_t 
         uint64_t n = (ngroups - done < cap) ? ngroups - done : cap;
         const uint64_t want = (n + kWaves - 1) / kWaves;
         const uint32_t grid = (uint32_t)(want < max_wgs ? want : max_wgs);
-        const uint8_t *b = base + done * nb_per_group * bs;
+        const uint8_t *b = base + done * nb_per_group * stride;
         uint32_t *o = out + done * nb_per_group;
         const uint32_t *img = ctx->d_lds_image[gi];
         const uint32_t *fold = (P.opt & 32) ? ctx->d_nibrep[log2u(P.G)] : ctx->d_fold + log2u(P.G) * 2048;
         // weights move whole groups: only worth it with many groups per wave
         uint32_t xw = n >= 32ull * grid * kWaves ? ctx->plan_xw[p] : 0u;
-        uint32_t tile = tile_groups(ctx, n, nb_per_group * bs);
-        void *args[] = {(void *)&b,    (void *)&n, (void *)&bs, (void *)&img, (void *)&fold,
-                        (void *)&o,    (void *)&xw, (void *)&tile};
+        uint32_t tile = tile_groups(ctx, n, nb_per_group * stride);
+        void *args[] = {(void *)&b, (void *)&n,  (void *)&bs,   (void *)&img,   (void *)&fold,
+                        (void *)&o, (void *)&xw, (void *)&tile, (void *)&stride};
         if (int rc = herr(hipLaunchKernel(plan_fn(p, ctx->prio), dim3(grid), dim3(kThreads), args, 0, s)))
             return rc;
         done += n;
@@ -547,7 +551,7 @@ uint32_t segments_for(const priskv_crc_ctx *ctx, uint64_t nblocks, uint32_t bs)
 }
 
 int launch_rows_plain(const priskv_crc_ctx *ctx, const uint8_t *base, uint64_t nblocks, uint32_t bs, uint32_t *out,
-                      hipStream_t s);
+                      hipStream_t s, uint32_t stride = 0);
 
 // Few extents: the same kernel over segments of each extent.  The segments
 // are laid out on the device by crc_seg_plan_kernel (the host never sees
@@ -710,20 +714,53 @@ int launch_rows(const priskv_crc_ctx *ctx, const uint8_t *base, uint64_t nblocks
 }
 
 int launch_rows_plain(const priskv_crc_ctx *ctx, const uint8_t *base, uint64_t nblocks, uint32_t bs, uint32_t *out,
-                      hipStream_t s)
+                      hipStream_t s, uint32_t stride)
 {
+    if (!stride)
+        stride = bs;
     const int p = plan_for(bs);
     const uint64_t per = 64 / kPlans[p].G; // blocks per wave group
     const uint64_t head = nblocks - nblocks % per;
     if (head)
-        if (int rc = launch_plan(ctx, p, base, head / per, bs, out, s))
+        if (int rc = launch_plan(ctx, p, base, head / per, bs, out, s, stride))
             return rc;
     if (head == nblocks)
         return 0;
     // ragged tail (< per blocks): one wave per block
     const uint32_t R = bs / PRV_ROW_BYTES;
     const int pt = R % 4 == 0 ? PLAN_G64_CH4 : (R % 2 == 0 ? PLAN_G64_CH2 : PLAN_G64_CH1);
-    return launch_plan(ctx, pt, base + head * (uint64_t)bs, nblocks - head, bs, out + head, s);
+    return launch_plan(ctx, pt, base + head * (uint64_t)stride, nblocks - head, bs, out + head, s, stride);
+}
+
+// ---- head-split blocks -------------------------------------------------------
+// A block size B that is a multiple of 4 with a small remainder over whole
+// KiB rows, B = h + body (h = B mod 1 KiB, 4 <= h <= kHeadMax, body >= 1
+// KiB), on a 4-byte aligned base: the rows kernel hashes the bodies in place
+// (stride B, 4-byte aligned loads stream at full rate) and crc_head_kernel
+// adds each head's term Z_body(crc(head)).  A 4096-B value with a 4-B
+// trailer, 4100 B, thus runs on the 4 KiB plan instead of the stride
+// kernel's 9 rows of 512 B for 4100 (12 % of them padding).  Batches that
+// would need segmenting (few large blocks) keep the stride / extents paths.
+// PRISKV_CRC_HEADSPLIT=0 turns it off.
+bool head_split(const priskv_crc_ctx *ctx, const void *base, uint64_t nblocks, uint32_t bs)
+{
+    const uint32_t h = bs % PRV_ROW_BYTES;
+    return (!ctx || ctx->head_split) && bs % 4 == 0 && ((uintptr_t)base & 3) == 0 && h >= 4 && h <= kHeadMax &&
+           bs - h >= PRV_ROW_BYTES && (!ctx || segments_for(ctx, nblocks, bs - h) == 1);
+}
+
+int launch_head_split(const priskv_crc_ctx *ctx, const uint8_t *base, uint64_t nblocks, uint32_t bs, uint32_t *out,
+                      hipStream_t s)
+{
+    const uint32_t h = bs % PRV_ROW_BYTES, body = bs - h;
+    if (int rc = launch_rows_plain(ctx, base + h, nblocks, body, out, s, bs))
+        return rc;
+    HeadCols z;
+    prv_shift_columns(z.c, body);
+    const uint64_t want = (nblocks + 255) / 256;
+    const uint32_t grid = (uint32_t)(want < (uint64_t)ctx->num_cus * 8 ? want : (uint64_t)ctx->num_cus * 8);
+    hipLaunchKernelGGL(crc_head_kernel, dim3(grid), dim3(256), 0, s, base, nblocks, bs, h, ctx->d_sarwate, z, out);
+    return herr(hipGetLastError());
 }
 
 // sub-KiB kernel for G = 1 << gl: bit-matrix fold at G = 1; for G >= 2 the
@@ -919,6 +956,8 @@ int launch_blocks(const priskv_crc_ctx *ctx, const uint8_t *base, uint64_t nbloc
     const int path = choose_path(base, bs, ctx->stride);
     if (path == PATH_ROWS)
         return launch_rows(ctx, base, nblocks, bs, out, s);
+    if (path == PATH_STRIDE && head_split(ctx, base, nblocks, bs))
+        return launch_head_split(ctx, base, nblocks, bs, out, s);
     if (path == PATH_STRIDE && !stride_to_extents(ctx, base, bs))
         return launch_stride(ctx, base, nblocks, bs, out, s);
     if (path == PATH_STRIDE) // odd blocks from 4.5 KiB, others from 9 KiB, beyond 64 MiB: extents (segmented when few)
@@ -1031,8 +1070,11 @@ int priskv_crc32_blocks_path(const void *d_base, uint64_t nblocks, uint32_t bloc
     if (block_size == 0 || (nblocks && !d_base))
         return -EINVAL;
     const int path = choose_path(d_base, block_size);
-    // a default context sends odd blocks from 4.5 KiB, other stride sizes
-    // from 9 KiB and blocks beyond 64 MiB to the extents kernel
+    // a default context hashes B = h + whole KiB rows as bodies + heads, and
+    // sends odd blocks from 4.5 KiB, other stride sizes from 9 KiB and blocks
+    // beyond 64 MiB to the extents kernel
+    if (path == PATH_STRIDE && head_split(nullptr, d_base, nblocks, block_size))
+        return PATH_HEAD;
     if (path == PATH_STRIDE && stride_to_extents_lim(d_base, block_size, kStrideOddMax, kStrideMax, true))
         return PATH_EXTENTS;
     return path;
@@ -1043,7 +1085,9 @@ int priskv_crc32_blocks_plan(const priskv_crc_ctx *ctx, const void *d_base, uint
 {
     if (!ctx || block_size == 0 || !buf || len == 0)
         return -EINVAL;
-    const int path = choose_path(d_base, block_size, ctx->stride);
+    int path = choose_path(d_base, block_size, ctx->stride);
+    if (path == PATH_STRIDE && head_split(ctx, d_base, nblocks, block_size))
+        path = PATH_HEAD;
     int w = 0;
     const char *fused_name = "crc_ranges_fused_kernel (few large values: segments, one launch)";
     if (path == PATH_STRIDE) {
@@ -1061,7 +1105,9 @@ int priskv_crc32_blocks_plan(const priskv_crc_ctx *ctx, const void *d_base, uint
         }
     } else if (path == PATH_ROWS && segments_for(ctx, nblocks, block_size) > 1 && fused_blocks(ctx, nblocks)) {
         w = snprintf(buf, len, "%s", fused_name);
-    } else if (path == PATH_ROWS) {
+    } else if (path == PATH_ROWS || path == PATH_HEAD) {
+        const uint32_t hb = path == PATH_HEAD ? block_size % PRV_ROW_BYTES : 0u; // head bytes
+        block_size -= hb;
         const uint32_t S = segments_for(ctx, nblocks, block_size);
         const uint32_t bs = block_size / S;
         const int p = plan_for(bs);
@@ -1082,6 +1128,8 @@ int priskv_crc32_blocks_plan(const priskv_crc_ctx *ctx, const void *d_base, uint
             w += snprintf(buf + w, len - w, ">%s", S > 1 ? " x segments + crc_combine_segments_kernel" : "");
         if (w >= 0 && (uint64_t)w < len && S > 1)
             w += snprintf(buf + w, len - w, " (%u segments of %u B per block)", S, bs);
+        if (w >= 0 && (uint64_t)w < len && hb)
+            w += snprintf(buf + w, len - w, " on the %u-B bodies + crc_head_kernel (%u-B heads)", block_size, hb);
     } else if (path == PATH_SMALL) {
         w = snprintf(buf, len, "crc_small_kernel<G=%u>", block_size / 16);
     } else if (path == PATH_EXTENTS) {
@@ -1129,6 +1177,8 @@ int priskv_crc_ctx_create(int device, priskv_crc_ctx **out)
         c->balance = !(be && !strcmp(be, "0"));
         const char *ea = getenv("PRISKV_CRC_EXT_ADAPT");
         c->ext_adapt = !(ea && !strcmp(ea, "0"));
+        const char *hs = getenv("PRISKV_CRC_HEADSPLIT");
+        c->head_split = !(hs && !strcmp(hs, "0"));
         const char *fc = getenv("PRISKV_CRC_FUSED_CH");
         c->fused_ch = fc ? atoi(fc) : kFusedCh;
         if (c->fused_ch != 2 && c->fused_ch != 4 && c->fused_ch != 8)

@@ -565,6 +565,35 @@ def test_ranges_many_per_wave_shapes(torch_cuda, any_ctx):
     assert np.array_equal(got, want), np.nonzero(got != want)[0][:8]
 
 
+@pytest.mark.parametrize("bs", [1028, 1024 + 64, 4100, 4104, 4096 + 64, 8196, (64 << 10) + 4, (1 << 20) + 4])
+def test_head_split_blocks(torch_cuda, ctx, bs):
+    """Block sizes of whole KiB rows plus a 4-64 B head on 4-byte aligned
+    bases: the rows kernel hashes the bodies in place (stride = block size)
+    and crc_head_kernel adds each head's shifted CRC.  Against the oracle on
+    every block, output pre-filled with a sentinel, at base offsets 0, 4 and
+    12, for ragged block counts (and few large blocks, which keep the other
+    paths), and against a context with the head split off."""
+    torch = torch_cuda
+    off_ctx = _ctx_env(PRISKV_CRC_HEADSPLIT=0)
+    sentinel = int(np.int32(np.uint32(0xA5A5A5A5).view(np.int32)))
+    for nb in sorted({1, 3, 65, 2049, max(1, (64 << 20) // bs) + 7}):
+        t = _region(torch, ctx, bs * nb + 16, SEED ^ (bs * 3 + nb), nb)
+        for shift in (0, 4, 12):
+            view = t[shift:shift + bs * nb]
+            plan = ctx.blocks_plan(view.data_ptr(), nb, bs)
+            want = O.crc32_blocks(view.cpu().numpy(), bs, nthreads=8)
+            for c in (ctx, off_ctx):
+                out = torch.full((nb,), sentinel, dtype=torch.int32, device="cuda")
+                c.blocks_dev(view, bs, out=out)
+                torch.cuda.synchronize()
+                got = _u32(out)
+                assert np.array_equal(got, want), (bs, nb, shift, plan, np.nonzero(got != want)[0][:8])
+        if nb >= 2049 and bs < (16 << 10):  # bodies too short to segment: always the head split
+            assert "crc_head_kernel" in ctx.blocks_plan(t.data_ptr(), nb, bs), plan
+        del t
+    off_ctx.close()
+
+
 def test_ranges_many_shape_chunk_sizes(torch_cuda, ctx):
     """The 16-wave many-extents shape sizes each wave's chunks from its own
     extents (8, 4 or 2 rows: crc_device.inc OPT bit 14).  Three populations
@@ -1043,15 +1072,20 @@ def test_blocks_plan_strings(torch_cuda, ctx):
     assert ctx.blocks_plan(base, 100, 256) == "crc_small_kernel<G=16>"
     # odd sizes and unaligned bases: the uniform-stride kernel
     assert ctx.blocks_plan(base + 1, 100, 4096).startswith("crc_stride_kernel<G=32,CH=8,NBUF=2,nt> (8 rows of 512 B")
-    assert ctx.blocks_plan(base, 100, 4100).startswith("crc_stride_kernel<G=32,CH=8,NBUF=2,nt> (9 rows of 512 B "
-                                                       "per block, 508 B in front)")
+    assert ctx.blocks_plan(base + 1, 100, 4100).startswith("crc_stride_kernel<G=32,CH=8,NBUF=2,nt> (9 rows of 512 B "
+                                                           "per block, 508 B in front)")
+    # whole KiB rows + a 4-64 B head on a 4-byte aligned base: rows kernel + head terms
+    assert ctx.blocks_plan(base, 100, 4100) == ("crc_rows_kernel<G=64,CH=4,NBUF=3,nt,pipelined-fold,nibble-fold,"
+                                                "progress-priority 3> on the 4096-B bodies + crc_head_kernel "
+                                                "(4-B heads)")
     assert ctx.blocks_plan(base, 100, 520).startswith("crc_stride_kernel<G=16,CH=8,NBUF=2,nt> (3 rows of 256 B")
     assert ctx.blocks_plan(base, 100, 100).startswith("crc_stride_kernel<G=8,CH=8,NBUF=2,nt> (1 rows of 128 B")
     # the extents kernel from 4.5 KiB for odd sizes, from 9 KiB for multiples of 4
     assert ctx.blocks_plan(base, 100, 4607).startswith("crc_stride_kernel<G=32,CH=8,NBUF=2,nt> (9 rows of 512 B")
     assert ctx.blocks_plan(base, 100, 4609) == "crc_ranges_kernel (extents)"
     assert ctx.blocks_plan(base, 100, 9212).startswith("crc_stride_kernel<G=32,CH=8,NBUF=2,nt> (18 rows of 512 B")
-    assert ctx.blocks_plan(base, 100, 9220) == "crc_ranges_kernel (extents)"
+    assert ctx.blocks_plan(base, 100, 9300) == "crc_ranges_kernel (extents)"
+    assert "crc_head_kernel (4-B heads)" in ctx.blocks_plan(base, 100, 9220)
     assert ctx.blocks_plan(base, 100, 15) == "crc_generic_kernel"
     off =_ctx_env(PRISKV_CRC_STRIDE="0")  # round 2's dispatch
     assert off.blocks_plan(base + 1, 100, 4096) == "crc_ranges_kernel (extents)"
@@ -1348,10 +1382,11 @@ def test_stride_kernel_every_g_and_shape(torch_cuda, G):
     3 and 4, for batches of 1 block, a ragged last group, and several groups
     per wave with a ragged end."""
     torch = torch_cuda
-    ctxs = [_ctx_env(PRISKV_CRC_STRIDE_G=G, PRISKV_CRC_STRIDE_SHAPE=sh) for sh in range(4)]
-    ctxs.append(_ctx_env(PRISKV_CRC_STRIDE_G=G, PRISKV_CRC_STRIDE_RUNS=1))  # G >= 16: groups in runs
-    ctxs.append(_ctx_env(PRISKV_CRC_STRIDE_G=G, PRISKV_CRC_STRIDE_FUNNEL=0))  # odd sizes: unaligned loads
-    ctxs.append(_ctx_env(PRISKV_CRC_STRIDE_G=G, PRISKV_CRC_STRIDE_MAX_KIB=131072))  # large blocks stay here
+    hs = {"PRISKV_CRC_HEADSPLIT": 0}  # 4100 B and the like stay on the stride kernel
+    ctxs = [_ctx_env(PRISKV_CRC_STRIDE_G=G, PRISKV_CRC_STRIDE_SHAPE=sh, **hs) for sh in range(4)]
+    ctxs.append(_ctx_env(PRISKV_CRC_STRIDE_G=G, PRISKV_CRC_STRIDE_RUNS=1, **hs))  # G >= 16: groups in runs
+    ctxs.append(_ctx_env(PRISKV_CRC_STRIDE_G=G, PRISKV_CRC_STRIDE_FUNNEL=0, **hs))  # odd sizes: unaligned loads
+    ctxs.append(_ctx_env(PRISKV_CRC_STRIDE_G=G, PRISKV_CRC_STRIDE_MAX_KIB=131072, **hs))  # large blocks stay here
     per = 64 // G
     rng = np.random.default_rng(G)
     try:
@@ -1435,20 +1470,22 @@ def test_stride_kernel_beyond_4GiB(torch_cuda, ctx):
                                                       False),
                                                      (4607, 6000, 1, "crc_stride_kernel<G=32,", False, False),
                                                      (4609, 6000, 0, "crc_ranges_kernel (extents)", False, False),
-                                                     (16388, 3000, 0, "crc_ranges_kernel (extents)", False, False),
-                                                     (4100, 2049, 4, "crc_stride_kernel<G=32,", False, False)])
+                                                     (16460, 3000, 0, "crc_ranges_kernel (extents)", False, False),
+                                                     (16388, 3000, 0, "crc_rows_kernel<G=64,", False, False),
+                                                     (4100, 2049, 4, "crc_rows_kernel<G=64,", False, False)])
 def test_stride_kernel_large_and_limit_blocks(torch_cuda, ctx, ctx_noseg, bs, nb, mis, kind, noseg, wide):
     """Blocks at both sides of the stride kernel's limits: 64 MiB (a few such
     blocks are cut into segments by the fused kernel, or with segmentation
     off and the size limit raised hashed whole by the stride kernel: 65 536
     rows of 1 KiB; more than 64 MiB keeps the extents path), 4.5 KiB for odd
     sizes and 9 KiB for multiples of 4 (the extents kernel from there), 2 GB
-    batches of 5 MiB + 8 / + 7 B blocks, and a batch whose last lane-group
-    runs are short: the oracle's CRCs."""
+    batches of 5 MiB + 8 / + 7 B blocks, a batch whose last lane-group runs
+    are short, and sizes of whole KiB rows + a 4-B head, which the head split
+    hands to the rows kernel: the oracle's CRCs."""
     torch = torch_cuda
     ctx = ctx_noseg if noseg else ctx
     if wide:
-        ctx = _ctx_env(PRISKV_CRC_SEGMENT="0", PRISKV_CRC_STRIDE_MAX_KIB=131072)
+        ctx = _ctx_env(PRISKV_CRC_SEGMENT="0", PRISKV_CRC_STRIDE_MAX_KIB=131072, PRISKV_CRC_HEADSPLIT=0)
     t = _region(torch, ctx, bs * nb + 16, SEED ^ (bs + nb), 5)
     view = t[mis: mis + bs * nb]
     plan = ctx.blocks_plan(view.data_ptr(), nb, bs)

@@ -227,7 +227,15 @@ def test_path_selection():
     assert C.blocks_path(4097, 10, 100) == "stride"
     assert C.blocks_path(4097, 10, 4096) == "stride"    # unaligned base
     assert C.blocks_path(4104, 10, 4096) == "stride"    # 8-byte aligned only
-    assert C.blocks_path(4096, 10, 4100) == "stride"    # not a multiple of 1 KiB
+    # whole KiB rows + a 4..64-B head (multiple of 4, 4-byte aligned base):
+    # the rows kernel on the bodies + crc_head_kernel
+    assert C.blocks_path(4096, 10, 4100) == "headsplit"
+    assert C.blocks_path(4100, 10, 4100) == "headsplit"   # 4-byte aligned base
+    assert C.blocks_path(4098, 10, 4100) == "stride"      # 2-byte aligned base
+    assert C.blocks_path(4096, 10, 1024 + 64) == "headsplit"
+    assert C.blocks_path(4096, 10, 1024 + 68) == "stride"  # head above 64 B
+    assert C.blocks_path(4096, 10, (64 << 10) + 4) == "headsplit"
+    assert C.blocks_path(4096, 10, 4097) == "stride"      # odd
     assert C.blocks_path(4096, 10, 1000) == "stride"
     assert C.blocks_path(4097, 10, 256) == "stride"     # sub-KiB power of two, unaligned base
     # the default limits hand larger stride sizes to the extents kernel
@@ -235,8 +243,8 @@ def test_path_selection():
     assert C.blocks_path(4096, 10, 4609) == "extents"   # odd from 4.5 KiB
     assert C.blocks_path(4097, 10, 8192) == "extents"   # unaligned base counts as odd
     assert C.blocks_path(4096, 10, 9212) == "stride"
-    assert C.blocks_path(4096, 10, 9220) == "extents"   # multiples of 4 from 9 KiB
-    assert C.blocks_path(4096, 10, (64 << 20) + 4) == "extents"
+    assert C.blocks_path(4096, 10, 9300) == "extents"   # multiples of 4 from 9 KiB (head 84 B)
+    assert C.blocks_path(4096, 10, (64 << 20) + 5) == "extents"
     assert C.blocks_path(4096, 10, 15) == "generic"     # below one 16-B window
     assert C.blocks_path(4096, 10, 1) == "generic"
 
