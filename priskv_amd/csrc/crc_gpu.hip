@@ -82,6 +82,8 @@ struct priskv_crc_ctx {
     uint32_t *d_fold;          // kFoldSets x 2048 words, set j for G = 1 << j
     uint32_t *d_nibrep[7];     // nibble fold tables for G = 1 << j (j >= 1), 8 x 16 x max(G, 32) words
     uint32_t *d_nib16;         // the extents kernel's: G = 16, width 16 (8 KiB)
+    uint32_t *d_small_img[5];  // sub-KiB byte-fold images for G = 1 << j, j = 1..4 (prv_small_image)
+    int small_bf;              // sub-KiB kernel folds through byte tables (PRISKV_CRC_SMALL_BF=0: nibble tables)
     uint32_t *d_sarwate;       // 256 words
     uint32_t *d_zpow;          // kZpowRows x 32 words: columns of Z_(2^k) (segment combine)
     uint32_t *d_rowshift;      // 16 x 4 x 32 words: columns of Z_-p o Z_(256(3-k)) (extents fold)
@@ -775,22 +777,27 @@ constexpr int kSmallOptPrio = 1 | (1 << 8) | 1024;
 // but at 182 VGPRs it halves the resident waves.
 constexpr int kSmallCh = 4, kSmallNbuf = 3, kSmallCh1 = 4, kSmallNbuf1 = 3;
 
+// byte-table fold (OPT bit 1) for G = 2..16: four lookups per fold instead
+// of eight nibble lookups (crc_device.inc byte_fold)
 template <int G>
-const void *small_fn_g(bool prio)
+const void *small_fn_g(bool prio, bool bf)
 {
+    if (bf && G <= 16)
+        return prio ? reinterpret_cast<const void *>(&crc_small_kernel<G, kSmallOptPrio | 2, kSmallCh, kSmallNbuf>)
+                    : reinterpret_cast<const void *>(&crc_small_kernel<G, 3>);
     return prio ? reinterpret_cast<const void *>(&crc_small_kernel<G, kSmallOptPrio, kSmallCh, kSmallNbuf>)
                 : reinterpret_cast<const void *>(&crc_small_kernel<G, 1>);
 }
 
-const void *small_fn(int gl, bool prio)
+const void *small_fn(int gl, bool prio, bool bf)
 {
     switch (gl) {
     case 0: return reinterpret_cast<const void *>(&crc_small_kernel<1, 0, kSmallCh1, kSmallNbuf1>);
-    case 1: return small_fn_g<2>(prio);
-    case 2: return small_fn_g<4>(prio);
-    case 3: return small_fn_g<8>(prio);
-    case 4: return small_fn_g<16>(prio);
-    default: return small_fn_g<32>(prio);
+    case 1: return small_fn_g<2>(prio, bf);
+    case 2: return small_fn_g<4>(prio, bf);
+    case 3: return small_fn_g<8>(prio, bf);
+    case 4: return small_fn_g<16>(prio, bf);
+    default: return small_fn_g<32>(prio, false);
     }
 }
 
@@ -883,9 +890,15 @@ constexpr int kStrideShape[4][2] = {{8, 2}, {4, 3}, {2, 4}, {4, 2}};
 // shape has a variant with aligned loads and funnel shifts; the
 // tuning shapes load at the unaligned rate
 template <int G>
-const void *stride_fn_g(int shape, bool odd)
+const void *stride_fn_g(int shape, bool odd, bool bf)
 {
     constexpr bool small = G < 16;
+    if constexpr (G <= 8) { // byte-table fold (R = 1: the B half of the image is free)
+        if (bf && odd && shape == 0)
+            return reinterpret_cast<const void *>(&crc_stride_kernel<G, 8, 2, kAux, true, true>);
+        if (bf && shape == 0)
+            return reinterpret_cast<const void *>(&crc_stride_kernel<G, 8, 2, kAux, false, true>);
+    }
     if (odd && shape == 0)
         return reinterpret_cast<const void *>(&crc_stride_kernel<G, 8, 2, kAux, true>);
     switch (shape) {
@@ -896,15 +909,15 @@ const void *stride_fn_g(int shape, bool odd)
     }
 }
 
-const void *stride_fn(int G, int shape, bool odd)
+const void *stride_fn(int G, int shape, bool odd, bool bf)
 {
     switch (G) {
-    case 2: return stride_fn_g<2>(shape, odd);
-    case 4: return stride_fn_g<4>(shape, odd);
-    case 8: return stride_fn_g<8>(shape, odd);
-    case 16: return stride_fn_g<16>(shape, odd);
-    case 32: return stride_fn_g<32>(shape, odd);
-    default: return stride_fn_g<64>(shape, odd);
+    case 2: return stride_fn_g<2>(shape, odd, bf);
+    case 4: return stride_fn_g<4>(shape, odd, bf);
+    case 8: return stride_fn_g<8>(shape, odd, bf);
+    case 16: return stride_fn_g<16>(shape, odd, false);
+    case 32: return stride_fn_g<32>(shape, odd, false);
+    default: return stride_fn_g<64>(shape, odd, false);
     }
 }
 
@@ -931,7 +944,10 @@ int launch_stride(const priskv_crc_ctx *ctx, const uint8_t *base, uint64_t nbloc
     // NB lane groups may run up to NB - 1 blocks past it: cap blocks per launch
     const uint64_t per_wave = ((1ull << 31) - 1) / bs - NB; // >= 1: bs <= kStrideMaxBlock
     const uint64_t cap = max_wgs * kWaves * per_wave;
-    const uint32_t *img = ctx->d_lds_image[P.G == 64 ? 0 : (P.G == 32 ? 1 : 2)]; // set B unused for G < 16 (R = 1)
+    // G <= 8 (R = 1, set B unused): the sub-KiB byte-fold image, no nibble tables
+    const bool bf = ctx->small_bf && P.G <= 8 && ctx->stride_shape == 0;
+    const uint32_t *img = bf ? ctx->d_small_img[log2u((uint32_t)P.G)]
+                             : ctx->d_lds_image[P.G == 64 ? 0 : (P.G == 32 ? 1 : 2)]; // set B unused for G < 16
     const uint32_t *nib = ctx->d_nibrep[log2u((uint32_t)P.G)];
     uint32_t R = P.R, runs = (uint32_t)ctx->stride_runs;
     for (uint64_t done = 0; done < nblocks;) {
@@ -939,7 +955,7 @@ int launch_stride(const priskv_crc_ctx *ctx, const uint8_t *base, uint64_t nbloc
         const uint64_t want = (nb + NB * kWaves - 1) / (NB * kWaves); // about NB blocks per wave and up
         const uint32_t grid = (uint32_t)(want < max_wgs ? want : max_wgs);
         const uint8_t *b = base + done * bs;
-        const void *fn = stride_fn(P.G, ctx->stride_shape, ctx->stride_funnel && (((uintptr_t)b | bs) & 3u));
+        const void *fn = stride_fn(P.G, ctx->stride_shape, ctx->stride_funnel && (((uintptr_t)b | bs) & 3u), bf);
         uint32_t *o = out + done;
         void *args[] = {(void *)&b,   (void *)&nb, (void *)&bs, (void *)&R,
                         (void *)&img, (void *)&nib, (void *)&o, (void *)&runs};
@@ -968,8 +984,9 @@ int launch_blocks(const priskv_crc_ctx *ctx, const uint8_t *base, uint64_t nbloc
         const uint64_t nrows = nblocks / per;
         if (nrows) {
             // G >= 2: nibble-table fold (replicated 32-wide tables)
+            const bool bf = ctx->small_bf && gl >= 1 && gl <= 4;
             const uint32_t *fold = gl ? ctx->d_nibrep[gl] : ctx->d_fold;
-            const uint32_t *img = ctx->d_lds_image[0];
+            const uint32_t *img = bf ? ctx->d_small_img[gl] : ctx->d_lds_image[0];
             const bool prio = gl && ctx->prio;
             const int waves = prio ? 2 * kWaves : kWaves;
             const uint64_t cap = prio ? (uint64_t)ctx->num_cus : (uint64_t)ctx->max_wgs;
@@ -977,7 +994,7 @@ int launch_blocks(const priskv_crc_ctx *ctx, const uint8_t *base, uint64_t nbloc
             const uint64_t want = (nrows + chw - 1) / chw;
             const uint32_t grid = (uint32_t)(want < cap ? want : cap);
             void *args[] = {(void *)&base, (void *)&nrows, (void *)&img, (void *)&fold, (void *)&out};
-            if (int rc = herr(hipLaunchKernel(small_fn(gl, prio), dim3(grid), dim3(64 * waves), args, 0, s)))
+            if (int rc = herr(hipLaunchKernel(small_fn(gl, prio, bf), dim3(grid), dim3(64 * waves), args, 0, s)))
                 return rc;
             if (int rc = herr(hipGetLastError()))
                 return rc;
@@ -1100,8 +1117,10 @@ int priskv_crc32_blocks_plan(const priskv_crc_ctx *ctx, const void *d_base, uint
             const int sh = ctx->stride_shape;
             const int ch = kStrideShape[sh][0];
             const int nbuf = sh == 1 ? (P.G < 16 ? 2 : 3) : (sh == 3 ? (P.G < 16 ? 3 : 2) : kStrideShape[sh][1]);
-            w = snprintf(buf, len, "crc_stride_kernel<G=%d,CH=%d,NBUF=%d,nt> (%u rows of %u B per block, %u B in front)",
-                         P.G, ch, nbuf, P.R, 16u * P.G, P.R * 16u * P.G - block_size);
+            const bool bf = ctx->small_bf && P.G <= 8 && sh == 0;
+            w = snprintf(buf, len,
+                         "crc_stride_kernel<G=%d,CH=%d,NBUF=%d,nt%s> (%u rows of %u B per block, %u B in front)", P.G,
+                         ch, nbuf, bf ? ",byte-fold" : "", P.R, 16u * P.G, P.R * 16u * P.G - block_size);
         }
     } else if (path == PATH_ROWS && segments_for(ctx, nblocks, block_size) > 1 && fused_blocks(ctx, nblocks)) {
         w = snprintf(buf, len, "%s", fused_name);
@@ -1131,7 +1150,8 @@ int priskv_crc32_blocks_plan(const priskv_crc_ctx *ctx, const void *d_base, uint
         if (w >= 0 && (uint64_t)w < len && hb)
             w += snprintf(buf + w, len - w, " on the %u-B bodies + crc_head_kernel (%u-B heads)", block_size, hb);
     } else if (path == PATH_SMALL) {
-        w = snprintf(buf, len, "crc_small_kernel<G=%u>", block_size / 16);
+        const uint32_t G = block_size / 16;
+        w = snprintf(buf, len, "crc_small_kernel<G=%u%s>", G, ctx->small_bf && G >= 2 && G <= 16 ? ",byte-fold" : "");
     } else if (path == PATH_EXTENTS) {
         w = snprintf(buf, len, "%s", extents_desc(ctx, nblocks, block_size));
     } else {
@@ -1179,6 +1199,8 @@ int priskv_crc_ctx_create(int device, priskv_crc_ctx **out)
         c->ext_adapt = !(ea && !strcmp(ea, "0"));
         const char *hs = getenv("PRISKV_CRC_HEADSPLIT");
         c->head_split = !(hs && !strcmp(hs, "0"));
+        const char *sb = getenv("PRISKV_CRC_SMALL_BF");
+        c->small_bf = !(sb && !strcmp(sb, "0"));
         const char *fc = getenv("PRISKV_CRC_FUSED_CH");
         c->fused_ch = fc ? atoi(fc) : kFusedCh;
         if (c->fused_ch != 2 && c->fused_ch != 4 && c->fused_ch != 8)
@@ -1253,6 +1275,15 @@ int priskv_crc_ctx_create(int device, priskv_crc_ctx **out)
             (rc = herr(hipMemcpy(c->d_nibrep[j], h_img, sizeof(uint32_t) * 8 * 16 * W, hipMemcpyHostToDevice))))
             goto fail;
     }
+    for (int j = 1; j <= 4; j++) {
+        const uint32_t G = 1u << j;
+        std::vector<uint32_t> simg(PRV_SMALL_WORDS(G));
+        prv_small_image(simg.data(), G);
+        if ((rc = herr(hipMalloc((void **)&c->d_small_img[j], sizeof(uint32_t) * simg.size()))) ||
+            (rc = herr(hipMemcpy(c->d_small_img[j], simg.data(), sizeof(uint32_t) * simg.size(),
+                                 hipMemcpyHostToDevice))))
+            goto fail;
+    }
     prv_fold_nibbles(h_img, 16, 16);
     if ((rc = herr(hipMalloc((void **)&c->d_nib16, sizeof(uint32_t) * 8 * 16 * 16))) ||
         (rc = herr(hipMemcpy(c->d_nib16, h_img, sizeof(uint32_t) * 8 * 16 * 16, hipMemcpyHostToDevice))))
@@ -1304,6 +1335,8 @@ void priskv_crc_ctx_destroy(priskv_crc_ctx *c)
     for (int j = 0; j < kFoldSets; j++)
         (void)hipFree(c->d_nibrep[j]);
     (void)hipFree(c->d_nib16);
+    for (int j = 1; j <= 4; j++)
+        (void)hipFree(c->d_small_img[j]);
     (void)hipFree(c->d_fold);
     (void)hipFree(c->d_sarwate);
     (void)hipFree(c->d_rowshift);

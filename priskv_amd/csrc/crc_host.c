@@ -204,6 +204,34 @@ void prv_fold_nibbles(uint32_t *out, uint32_t group, uint32_t width)
     }
 }
 
+void prv_small_image(uint32_t *out, uint32_t group)
+{
+    /* set A (Z_4) as prv_lds_image; fold entry F_j[b][c] = Z_(4 + 16(G-1-c))(b << 8j)
+     * at word region(j)*PRV_LDS_WORDS + b*64 + 32 + e (layout: crc_device.inc fold_const) */
+    const uint32_t G = group;
+    uint32_t za[32];
+    prv_shift_columns(za, 4);
+    memset(out, 0, sizeof(uint32_t) * PRV_SMALL_WORDS(G));
+    for (uint32_t b = 0; b < 256; b++)
+        for (uint32_t k = 0; k < 8; k++)
+            for (uint32_t t = 0; t < 4; t++)
+                out[b * 64 + 4 * k + t] = mat_apply(za, b << (8 * t));
+    for (uint32_t c = 0; c < G; c++) {
+        uint32_t zc[32];
+        prv_shift_columns(zc, 4ull + 16ull * (G - 1 - c));
+        for (uint32_t j = 0; j < 4; j++)
+            for (uint32_t b = 0; b < 256; b++) {
+                const uint32_t v = mat_apply(zc, b << (8 * j));
+                if (G == 16) {
+                    out[(j >> 1) * PRV_LDS_WORDS + b * 64 + 32 + 16 * (j & 1) + c] = v;
+                } else {
+                    for (uint32_t cp = 0; cp < 8 / G; cp++)
+                        out[b * 64 + 32 + cp * 4 * G + j * G + c] = v;
+                }
+            }
+    }
+}
+
 /* one zero byte backwards: c' = T[c & 0xff] ^ (c >> 8) has top byte
  * T[c & 0xff] >> 24, and the top bytes of the 256 table entries are distinct,
  * so c & 0xff = b with T[b] >> 24 == c' >> 24 and c = ((c' ^ T[b]) << 8) | b */

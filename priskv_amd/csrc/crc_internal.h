@@ -26,6 +26,12 @@ PRV_HIDDEN void prv_fold_columns(uint32_t out[32 * 64], uint32_t group);
 /* nibble fold tables, 8*16*width words (crc_device.inc nib_fold) */
 PRV_HIDDEN void prv_fold_nibbles(uint32_t *out, uint32_t group, uint32_t width);
 PRV_HIDDEN void prv_shift_columns(uint32_t out[32], uint64_t nbytes);
+/* sub-KiB byte-fold image for G = 2..16 lanes per block (crc_device.inc
+ * byte_fold): set A of prv_lds_image in words [0,32) of each 64-word row,
+ * the byte fold tables in words [32,64); G = 16 adds a second 64 KiB region
+ * (tables of bytes 2, 3).  PRV_SMALL_WORDS(G) words. */
+#define PRV_SMALL_WORDS(G) ((G) == 16 ? 2 * PRV_LDS_WORDS : PRV_LDS_WORDS)
+PRV_HIDDEN void prv_small_image(uint32_t *out, uint32_t group);
 PRV_HIDDEN void prv_sarwate_table(uint32_t out[256]);
 /* host CRC register update (init = crc, no xor): tables; clmul folding for
  * len >= 64 / vclmul for len >= 256 (x86-64, after prv_clmul_init) */

@@ -216,6 +216,30 @@ def test_blocks_vs_oracle(torch_cuda, ctx, bs):
         assert np.array_equal(got, want), (bs, nb, np.nonzero(got != want)[0][:8])
 
 
+@pytest.mark.parametrize("bf", ["1", "0"])
+def test_sub_kib_fold_tables(torch_cuda, bf):
+    """crc_small_kernel with the byte-table fold (default) and the nibble
+    fold (PRISKV_CRC_SMALL_BF=0) against the oracle, every sub-KiB power of
+    two, whole and ragged rows (the ragged tail takes the generic kernel)."""
+    torch = torch_cuda
+    c = _ctx_env(PRISKV_CRC_SMALL_BF=bf)
+    try:
+        for bs in (16, 32, 64, 128, 256, 512):
+            plan = c.blocks_plan(16, 4096, bs)
+            assert plan.startswith(f"crc_small_kernel<G={bs // 16}"), plan
+            assert ("byte-fold" in plan) == (bf == "1" and 32 <= bs <= 256), plan
+            for nb in (1024 // bs * 3 * 2048 * 16 + 1, 1024 // bs * 40 + 3):
+                t = _region(torch, c, bs * nb, SEED ^ (bs * 7 + nb), nb)
+                out = torch.full((nb,), 0x5A5A5A5A, dtype=torch.int32, device="cuda")
+                got = _u32(c.blocks_dev(t, bs, out=out, nblocks=nb))
+                torch.cuda.synchronize()
+                want = O.crc32_blocks(t[: bs * nb].cpu().numpy(), bs, nthreads=8)
+                assert np.array_equal(got, want), (bf, bs, nb, np.nonzero(got != want)[0][:8])
+                del t
+    finally:
+        c.close()
+
+
 @pytest.mark.parametrize("misalign", [1, 2, 4, 8, 12, 15])
 @pytest.mark.parametrize("bs", [4096, 1000, 4100])
 def test_unaligned_base(torch_cuda, ctx, misalign, bs):
@@ -1069,7 +1093,7 @@ def test_blocks_plan_strings(torch_cuda, ctx):
     assert ctx.blocks_plan(base, 20000, 1 << 20).startswith("crc_rows_kernel")  # balanced: whole blocks
     # more than 64 unbalanced large blocks: rows kernel on segments + combine
     assert "crc_combine_segments_kernel" in ctx.blocks_plan(base, 1000, 1 << 20)
-    assert ctx.blocks_plan(base, 100, 256) == "crc_small_kernel<G=16>"
+    assert ctx.blocks_plan(base, 100, 256) == "crc_small_kernel<G=16,byte-fold>"
     # odd sizes and unaligned bases: the uniform-stride kernel
     assert ctx.blocks_plan(base + 1, 100, 4096).startswith("crc_stride_kernel<G=32,CH=8,NBUF=2,nt> (8 rows of 512 B")
     assert ctx.blocks_plan(base + 1, 100, 4100).startswith("crc_stride_kernel<G=32,CH=8,NBUF=2,nt> (9 rows of 512 B "
@@ -1079,7 +1103,7 @@ def test_blocks_plan_strings(torch_cuda, ctx):
                                                 "progress-priority 3> on the 4096-B bodies + crc_head_kernel "
                                                 "(4-B heads)")
     assert ctx.blocks_plan(base, 100, 520).startswith("crc_stride_kernel<G=16,CH=8,NBUF=2,nt> (3 rows of 256 B")
-    assert ctx.blocks_plan(base, 100, 100).startswith("crc_stride_kernel<G=8,CH=8,NBUF=2,nt> (1 rows of 128 B")
+    assert ctx.blocks_plan(base, 100, 100).startswith("crc_stride_kernel<G=8,CH=8,NBUF=2,nt,byte-fold> (1 rows of 128 B")
     # the extents kernel from 4.5 KiB for odd sizes, from 9 KiB for multiples of 4
     assert ctx.blocks_plan(base, 100, 4607).startswith("crc_stride_kernel<G=32,CH=8,NBUF=2,nt> (9 rows of 512 B")
     assert ctx.blocks_plan(base, 100, 4609) == "crc_ranges_kernel (extents)"
@@ -1387,6 +1411,7 @@ def test_stride_kernel_every_g_and_shape(torch_cuda, G):
     ctxs.append(_ctx_env(PRISKV_CRC_STRIDE_G=G, PRISKV_CRC_STRIDE_RUNS=1, **hs))  # G >= 16: groups in runs
     ctxs.append(_ctx_env(PRISKV_CRC_STRIDE_G=G, PRISKV_CRC_STRIDE_FUNNEL=0, **hs))  # odd sizes: unaligned loads
     ctxs.append(_ctx_env(PRISKV_CRC_STRIDE_G=G, PRISKV_CRC_STRIDE_MAX_KIB=131072, **hs))  # large blocks stay here
+    ctxs.insert(1, _ctx_env(PRISKV_CRC_STRIDE_G=G, PRISKV_CRC_SMALL_BF=0, **hs))  # G <= 8: nibble fold
     per = 64 // G
     rng = np.random.default_rng(G)
     try:

@@ -22,6 +22,8 @@
 #   ktracepy:SCRIPT[:A,B] rocprofv3 --kernel-trace --stats over python tools/SCRIPT A B ...
 #   pmc:C1+C2[:A,B,...]   one rocprofv3 --pmc pass (counters C1 C2 ...) over bench.py A B ...
 #   pmcpy:C1+C2:SCRIPT[:A,B]  one --pmc pass over python tools/SCRIPT A B ...
+#   pmclib:C1+C2:ARGS     one --pmc pass over tools/lib_timing ARGS (no torch in the process)
+#   ktracelib:ARGS        rocprofv3 --kernel-trace --stats over tools/lib_timing ARGS
 #   oversub               bench.py as 2 ranks on this one GPU WITHOUT the rehearsal
 #                         variable: must exit 3 (the device guard) -- the step fails otherwise
 set -euo pipefail
@@ -124,6 +126,19 @@ for step in "$@"; do
         (cd /tmp && export TMPDIR=/tmp &&
             timeout -s KILL 180 rocprofv3 --pmc ${ctrs//+/ } -d "$O/pmcpy_$n" -o run --output-format csv \
                 -- python3 "$R/tools/$script" ${pargs//,/ } > "$O/pmcpy_$n.out" 2> "$O/pmcpy_$n.err")
+        ;;
+    pmclib)
+        ctrs=${arg%%:*}
+        largs=""
+        [[ "$arg" == *:* ]] && largs=${arg#*:}
+        (cd /tmp && export TMPDIR=/tmp &&
+            timeout -s KILL 120 rocprofv3 --pmc ${ctrs//+/ } -d "$O/pmclib_$n" -o run --output-format csv \
+                -- "$R/tools/lib_timing" ${largs//,/ } > "$O/pmclib_$n.out" 2> "$O/pmclib_$n.err")
+        ;;
+    ktracelib)
+        (cd /tmp && export TMPDIR=/tmp &&
+            timeout -k 10 200 rocprofv3 --kernel-trace --stats -d "$O/ktracelib_$n" -o run --output-format csv \
+                -- "$R/tools/lib_timing" ${arg//,/ } > "$O/ktracelib_$n.out" 2> "$O/ktracelib_$n.err")
         ;;
     *)
         echo "unknown step $step" >&2
