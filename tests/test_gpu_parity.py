@@ -228,7 +228,7 @@ def test_sub_kib_fold_tables(torch_cuda, bf):
             plan = c.blocks_plan(16, 4096, bs)
             assert plan.startswith(f"crc_small_kernel<G={bs // 16}"), plan
             assert ("byte-fold" in plan) == (bf == "1" and 32 <= bs <= 256), plan
-            for nb in (1024 // bs * 3 * 2048 * 16 + 1, 1024 // bs * 40 + 3):
+            for nb in (1024 // bs * 3 * 2048 * 16 + 1, 1024 // bs * 40 + 3, 1024 // bs * 256 * 16 * 4 * 5 + 7):
                 t = _region(torch, c, bs * nb, SEED ^ (bs * 7 + nb), nb)
                 out = torch.full((nb,), 0x5A5A5A5A, dtype=torch.int32, device="cuda")
                 got = _u32(c.blocks_dev(t, bs, out=out, nblocks=nb))

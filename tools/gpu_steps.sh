@@ -23,6 +23,7 @@
 #   pmc:C1+C2[:A,B,...]   one rocprofv3 --pmc pass (counters C1 C2 ...) over bench.py A B ...
 #   pmcpy:C1+C2:SCRIPT[:A,B]  one --pmc pass over python tools/SCRIPT A B ...
 #   pmclib:C1+C2:ARGS     one --pmc pass over tools/lib_timing ARGS (no torch in the process)
+#   pmcprobe:C1+C2:ARGS   one --pmc pass over tools/alloc_probe ARGS
 #   ktracelib:ARGS        rocprofv3 --kernel-trace --stats over tools/lib_timing ARGS
 #   oversub               bench.py as 2 ranks on this one GPU WITHOUT the rehearsal
 #                         variable: must exit 3 (the device guard) -- the step fails otherwise
@@ -134,6 +135,14 @@ for step in "$@"; do
         (cd /tmp && export TMPDIR=/tmp &&
             timeout -s KILL 120 rocprofv3 --pmc ${ctrs//+/ } -d "$O/pmclib_$n" -o run --output-format csv \
                 -- "$R/tools/lib_timing" ${largs//,/ } > "$O/pmclib_$n.out" 2> "$O/pmclib_$n.err")
+        ;;
+    pmcprobe)
+        ctrs=${arg%%:*}
+        largs=""
+        [[ "$arg" == *:* ]] && largs=${arg#*:}
+        (cd /tmp && export TMPDIR=/tmp &&
+            timeout -s KILL 120 rocprofv3 --pmc ${ctrs//+/ } -d "$O/pmcprobe_$n" -o run --output-format csv \
+                -- "$R/tools/alloc_probe" ${largs//,/ } > "$O/pmcprobe_$n.out" 2> "$O/pmcprobe_$n.err")
         ;;
     ktracelib)
         (cd /tmp && export TMPDIR=/tmp &&
