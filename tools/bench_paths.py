@@ -255,6 +255,9 @@ def main():
             if bs in (100, 4100):
                 total = 64 << 20
             blocks_case(ctx, bs, total)
+    if "paths1g" in which:  # DESIGN §6 "Other paths": 1 GiB per call, every non-headline block plan
+        for bs in (4096, 4096, 16, 32, 64, 128, 256, 512, 100, 1000, 1023, 2047, 4095, 4097, 4100, 12345, 65537):
+            blocks_case(ctx, bs, 1 << 30)
     if "ranges" in which:
         ranges_dev_case(ctx)
         ranges_dev_case(ctx, bs=65536, n=1 << 15)
