@@ -181,8 +181,7 @@ int priskv_crc_fill_splitmix_dev(const priskv_crc_ctx *ctx, void *d_dst, uint64_
  * 16-byte aligned base: G = 16/32/64 lanes per block; batches of few large
  * blocks are hashed as segments and combined), 3 = sub-KiB power-of-two
  * blocks (16-byte aligned base), 5 = uniform stride (any other block of
- * 16 B up to 4.5 KiB when the size or base is not a multiple of 4, up to
- * 9 KiB otherwise: rows aligned to each block's end), 2 = extents (the
+ * 16 B up to 9 KiB: rows aligned to each block's end), 2 = extents (the
  * larger such blocks, and every block beyond 64 MiB), 4 = generic (blocks
  * below 16 B: one thread per block), 6 = head split (a multiple of 4 that is
  * whole KiB rows plus a 4-64 B head, 4-byte aligned base: the rows kernel on

@@ -84,6 +84,7 @@ struct priskv_crc_ctx {
     uint32_t *d_nib16;         // the extents kernel's: G = 16, width 16 (8 KiB)
     uint32_t *d_small_img[5];  // sub-KiB byte-fold images for G = 1 << j, j = 1..4 (prv_small_image)
     int small_bf;              // sub-KiB kernel folds through byte tables (PRISKV_CRC_SMALL_BF=0: nibble tables)
+    int stride_prio;           // stride kernel (G >= 16): progress-priority mode in one 16-wave workgroup per CU
     uint32_t *d_sarwate;       // 256 words
     uint32_t *d_zpow;          // kZpowRows x 32 words: columns of Z_(2^k) (segment combine)
     uint32_t *d_rowshift;      // 16 x 4 x 32 words: columns of Z_-p o Z_(256(3-k)) (extents fold)
@@ -824,9 +825,13 @@ constexpr uint32_t kStrideMaxBlock = 64u << 20; // larger odd blocks keep the (s
 // 8196 B 5.83 / 5.92 (sweep_cross), 10 244 B 6.22 / 6.01, 14 340 B 6.42 /
 // 5.99, 32 772 B 6.62 / 6.18 (profiles/r02/stride/).  The limits sit midway
 // between the last size the stride kernel led and the first it did not.
+// Round 3: with progress priority in one 16-wave workgroup the stride kernel
+// leads odd sizes up to 8.5 KiB (4609 B 5.84 / 5.19 extents, 8193 B 6.10 /
+// 5.70, 8705 B 6.01 / 5.88) and trails from 9 KiB (9217 B 6.04 / 6.11,
+// 10 241 B 6.01 / 6.37; profiles/r03/stride_prio/), so both limits are 9 KiB.
 // PRISKV_CRC_STRIDE_MAX_KIB sets both (tuning, and the tests of the
 // kernel's large-block limits).
-constexpr uint32_t kStrideOddMax = 4608;
+constexpr uint32_t kStrideOddMax = 9u << 10;
 constexpr uint32_t kStrideMax = 9u << 10;
 
 bool stride_to_extents_lim(const void *base, uint32_t bs, uint64_t odd_max, uint64_t max, bool funnel)
@@ -890,9 +895,20 @@ constexpr int kStrideShape[4][2] = {{8, 2}, {4, 3}, {2, 4}, {4, 2}};
 // shape has a variant with aligned loads and funnel shifts; the
 // tuning shapes load at the unaligned rate
 template <int G>
-const void *stride_fn_g(int shape, bool odd, bool bf)
+const void *stride_fn_g(int shape, bool odd, bool bf, int prio)
 {
     constexpr bool small = G < 16;
+    // one 16-wave workgroup per CU with progress-priority mode 3 (default
+    // shape; G <= 8 with the byte fold)
+    if constexpr (G >= 16) {
+        if (prio && shape == 0)
+            return odd ? reinterpret_cast<const void *>(&crc_stride_kernel<G, 8, 2, kAux, true, false, 3>)
+                       : reinterpret_cast<const void *>(&crc_stride_kernel<G, 8, 2, kAux, false, false, 3>);
+    } else {
+        if (prio && bf && shape == 0)
+            return odd ? reinterpret_cast<const void *>(&crc_stride_kernel<G, 8, 2, kAux, true, true, 3>)
+                       : reinterpret_cast<const void *>(&crc_stride_kernel<G, 8, 2, kAux, false, true, 3>);
+    }
     if constexpr (G <= 8) { // byte-table fold (R = 1: the B half of the image is free)
         if (bf && odd && shape == 0)
             return reinterpret_cast<const void *>(&crc_stride_kernel<G, 8, 2, kAux, true, true>);
@@ -909,25 +925,40 @@ const void *stride_fn_g(int shape, bool odd, bool bf)
     }
 }
 
-const void *stride_fn(int G, int shape, bool odd, bool bf)
+const void *stride_fn(int G, int shape, bool odd, bool bf, int prio)
 {
     switch (G) {
-    case 2: return stride_fn_g<2>(shape, odd, bf);
-    case 4: return stride_fn_g<4>(shape, odd, bf);
-    case 8: return stride_fn_g<8>(shape, odd, bf);
-    case 16: return stride_fn_g<16>(shape, odd, false);
-    case 32: return stride_fn_g<32>(shape, odd, false);
-    default: return stride_fn_g<64>(shape, odd, false);
+    case 2: return stride_fn_g<2>(shape, odd, bf, prio);
+    case 4: return stride_fn_g<4>(shape, odd, bf, prio);
+    case 8: return stride_fn_g<8>(shape, odd, bf, prio);
+    case 16: return stride_fn_g<16>(shape, odd, false, prio);
+    case 32: return stride_fn_g<32>(shape, odd, false, prio);
+    default: return stride_fn_g<64>(shape, odd, false, prio);
     }
 }
 
 // Few large odd blocks: the stride kernel splits groups statically like the
 // rows kernel, so an unbalanced handful of big blocks goes to the fused
 // few-extents kernel, which cuts them into segments (as launch_rows does)
+// G <= 8 (R = 1, set B unused): the sub-KiB byte-fold image, no nibble tables
+bool stride_bf(const priskv_crc_ctx *ctx, int G) { return ctx->small_bf && G <= 8 && ctx->stride_shape == 0; }
+
+// progress priority (mode, 0 = off): one 16-wave workgroup per CU, default
+// shape; G <= 8 only with the byte fold, whose tables fit the 64 KiB image
+int stride_prio_mode(const priskv_crc_ctx *ctx, int G)
+{
+    return (ctx->stride_shape == 0 && (G >= 16 || stride_bf(ctx, G))) ? ctx->stride_prio : 0;
+}
+
+uint64_t stride_waves(const priskv_crc_ctx *ctx, int G)
+{
+    return stride_prio_mode(ctx, G) ? (uint64_t)ctx->num_cus * 16 : (uint64_t)ctx->num_cus * stride_wgs(ctx, G) * kWaves;
+}
+
 bool stride_segmented(const priskv_crc_ctx *ctx, const StridePlan &P, uint64_t nblocks, uint32_t bs)
 {
     const uint64_t NB = 64 / (uint64_t)P.G;
-    const uint64_t waves = (uint64_t)ctx->num_cus * stride_wgs(ctx, P.G) * kWaves;
+    const uint64_t waves = stride_waves(ctx, P.G);
     return ctx->segment && ctx->fused && bs >= kSegMinLen && nblocks <= kFusedMaxExtents &&
            !balanced((nblocks + NB - 1) / NB, waves);
 }
@@ -939,27 +970,28 @@ int launch_stride(const priskv_crc_ctx *ctx, const uint8_t *base, uint64_t nbloc
     if (stride_segmented(ctx, P, nblocks, bs))
         return launch_fused(ctx, base, nblocks, nullptr, nullptr, bs, bs, out, s);
     const uint64_t NB = 64 / (uint64_t)P.G;
-    const uint64_t max_wgs = (uint64_t)ctx->num_cus * stride_wgs(ctx, P.G);
+    const bool bf = stride_bf(ctx, P.G);
+    const int prio = stride_prio_mode(ctx, P.G);
+    const uint64_t nw = prio ? 16 : kWaves;
+    const uint64_t max_wgs = prio ? (uint64_t)ctx->num_cus : (uint64_t)ctx->num_cus * stride_wgs(ctx, P.G);
     // a wave's range is one buffer descriptor with 31-bit offsets, and its
     // NB lane groups may run up to NB - 1 blocks past it: cap blocks per launch
     const uint64_t per_wave = ((1ull << 31) - 1) / bs - NB; // >= 1: bs <= kStrideMaxBlock
-    const uint64_t cap = max_wgs * kWaves * per_wave;
-    // G <= 8 (R = 1, set B unused): the sub-KiB byte-fold image, no nibble tables
-    const bool bf = ctx->small_bf && P.G <= 8 && ctx->stride_shape == 0;
+    const uint64_t cap = max_wgs * nw * per_wave;
     const uint32_t *img = bf ? ctx->d_small_img[log2u((uint32_t)P.G)]
                              : ctx->d_lds_image[P.G == 64 ? 0 : (P.G == 32 ? 1 : 2)]; // set B unused for G < 16
     const uint32_t *nib = ctx->d_nibrep[log2u((uint32_t)P.G)];
     uint32_t R = P.R, runs = (uint32_t)ctx->stride_runs;
     for (uint64_t done = 0; done < nblocks;) {
         uint64_t nb = nblocks - done < cap ? nblocks - done : cap;
-        const uint64_t want = (nb + NB * kWaves - 1) / (NB * kWaves); // about NB blocks per wave and up
+        const uint64_t want = (nb + NB * nw - 1) / (NB * nw); // about NB blocks per wave and up
         const uint32_t grid = (uint32_t)(want < max_wgs ? want : max_wgs);
         const uint8_t *b = base + done * bs;
-        const void *fn = stride_fn(P.G, ctx->stride_shape, ctx->stride_funnel && (((uintptr_t)b | bs) & 3u), bf);
+        const void *fn = stride_fn(P.G, ctx->stride_shape, ctx->stride_funnel && (((uintptr_t)b | bs) & 3u), bf, prio);
         uint32_t *o = out + done;
         void *args[] = {(void *)&b,   (void *)&nb, (void *)&bs, (void *)&R,
                         (void *)&img, (void *)&nib, (void *)&o, (void *)&runs};
-        if (int rc = herr(hipLaunchKernel(fn, dim3(grid), dim3(kThreads), args, 0, s)))
+        if (int rc = herr(hipLaunchKernel(fn, dim3(grid), dim3(64 * nw), args, 0, s)))
             return rc;
         done += nb;
     }
@@ -1117,10 +1149,12 @@ int priskv_crc32_blocks_plan(const priskv_crc_ctx *ctx, const void *d_base, uint
             const int sh = ctx->stride_shape;
             const int ch = kStrideShape[sh][0];
             const int nbuf = sh == 1 ? (P.G < 16 ? 2 : 3) : (sh == 3 ? (P.G < 16 ? 3 : 2) : kStrideShape[sh][1]);
-            const bool bf = ctx->small_bf && P.G <= 8 && sh == 0;
+            const bool bf = stride_bf(ctx, P.G);
+            const int pm = stride_prio_mode(ctx, P.G);
             w = snprintf(buf, len,
-                         "crc_stride_kernel<G=%d,CH=%d,NBUF=%d,nt%s> (%u rows of %u B per block, %u B in front)", P.G,
-                         ch, nbuf, bf ? ",byte-fold" : "", P.R, 16u * P.G, P.R * 16u * P.G - block_size);
+                         "crc_stride_kernel<G=%d,CH=%d,NBUF=%d,nt%s%s> (%u rows of %u B per block, %u B in front)",
+                         P.G, ch, nbuf, bf ? ",byte-fold" : "", pm ? ",progress-priority 3" : "", P.R, 16u * P.G,
+                         P.R * 16u * P.G - block_size);
         }
     } else if (path == PATH_ROWS && segments_for(ctx, nblocks, block_size) > 1 && fused_blocks(ctx, nblocks)) {
         w = snprintf(buf, len, "%s", fused_name);
@@ -1226,6 +1260,9 @@ int priskv_crc_ctx_create(int device, priskv_crc_ctx **out)
         if (const char *m = getenv("PRISKV_CRC_STRIDE_MAX_KIB"))
             c->stride_max = c->stride_odd_max = strtoull(m, nullptr, 10) << 10;
         c->stride_wgs = 2;
+        c->stride_prio = c->prio ? 3 : 0; // PRISKV_CRC_PRIO=0 turns it off with the others
+        if (const char *m = getenv("PRISKV_CRC_STRIDE_PRIO"))
+            c->stride_prio = atoi(m) ? 3 : 0;
         if (const char *m = getenv("PRISKV_CRC_STRIDE_WGS"))
             c->stride_wgs = atoi(m) == 1 ? 1 : 2;
         c->seg_max_extents = kSegMaxExtents;

@@ -1095,19 +1095,21 @@ def test_blocks_plan_strings(torch_cuda, ctx):
     assert "crc_combine_segments_kernel" in ctx.blocks_plan(base, 1000, 1 << 20)
     assert ctx.blocks_plan(base, 100, 256) == "crc_small_kernel<G=16,byte-fold>"
     # odd sizes and unaligned bases: the uniform-stride kernel
-    assert ctx.blocks_plan(base + 1, 100, 4096).startswith("crc_stride_kernel<G=32,CH=8,NBUF=2,nt> (8 rows of 512 B")
-    assert ctx.blocks_plan(base + 1, 100, 4100).startswith("crc_stride_kernel<G=32,CH=8,NBUF=2,nt> (9 rows of 512 B "
+    assert ctx.blocks_plan(base + 1, 100, 4096).startswith("crc_stride_kernel<G=32,CH=8,NBUF=2,nt,progress-priority 3> (8 rows of 512 B")
+    assert ctx.blocks_plan(base + 1, 100, 4100).startswith("crc_stride_kernel<G=32,CH=8,NBUF=2,nt,progress-priority 3> "
+                                                           "(9 rows of 512 B "
                                                            "per block, 508 B in front)")
     # whole KiB rows + a 4-64 B head on a 4-byte aligned base: rows kernel + head terms
     assert ctx.blocks_plan(base, 100, 4100) == ("crc_rows_kernel<G=64,CH=4,NBUF=3,nt,pipelined-fold,nibble-fold,"
                                                 "progress-priority 3> on the 4096-B bodies + crc_head_kernel "
                                                 "(4-B heads)")
-    assert ctx.blocks_plan(base, 100, 520).startswith("crc_stride_kernel<G=16,CH=8,NBUF=2,nt> (3 rows of 256 B")
-    assert ctx.blocks_plan(base, 100, 100).startswith("crc_stride_kernel<G=8,CH=8,NBUF=2,nt,byte-fold> (1 rows of 128 B")
-    # the extents kernel from 4.5 KiB for odd sizes, from 9 KiB for multiples of 4
-    assert ctx.blocks_plan(base, 100, 4607).startswith("crc_stride_kernel<G=32,CH=8,NBUF=2,nt> (9 rows of 512 B")
-    assert ctx.blocks_plan(base, 100, 4609) == "crc_ranges_kernel (extents)"
-    assert ctx.blocks_plan(base, 100, 9212).startswith("crc_stride_kernel<G=32,CH=8,NBUF=2,nt> (18 rows of 512 B")
+    assert ctx.blocks_plan(base, 100, 520).startswith("crc_stride_kernel<G=16,CH=8,NBUF=2,nt,progress-priority 3> (3 rows of 256 B")
+    assert ctx.blocks_plan(base, 100, 100).startswith("crc_stride_kernel<G=8,CH=8,NBUF=2,nt,byte-fold,progress-priority 3> (1 rows of 128 B")
+    # the extents kernel from 9 KiB, odd sizes and multiples of 4 alike
+    assert ctx.blocks_plan(base, 100, 4609).startswith("crc_stride_kernel<G=32,CH=8,NBUF=2,nt,progress-priority 3>")
+    assert ctx.blocks_plan(base, 100, 9215).startswith("crc_stride_kernel<")
+    assert ctx.blocks_plan(base, 100, 9217) == "crc_ranges_kernel (extents)"
+    assert ctx.blocks_plan(base, 100, 9212).startswith("crc_stride_kernel<G=32,CH=8,NBUF=2,nt,progress-priority 3> (18 rows of 512 B")
     assert ctx.blocks_plan(base, 100, 9300) == "crc_ranges_kernel (extents)"
     assert "crc_head_kernel (4-B heads)" in ctx.blocks_plan(base, 100, 9220)
     assert ctx.blocks_plan(base, 100, 15) == "crc_generic_kernel"
@@ -1412,6 +1414,7 @@ def test_stride_kernel_every_g_and_shape(torch_cuda, G):
     ctxs.append(_ctx_env(PRISKV_CRC_STRIDE_G=G, PRISKV_CRC_STRIDE_FUNNEL=0, **hs))  # odd sizes: unaligned loads
     ctxs.append(_ctx_env(PRISKV_CRC_STRIDE_G=G, PRISKV_CRC_STRIDE_MAX_KIB=131072, **hs))  # large blocks stay here
     ctxs.insert(1, _ctx_env(PRISKV_CRC_STRIDE_G=G, PRISKV_CRC_SMALL_BF=0, **hs))  # G <= 8: nibble fold
+    ctxs.insert(2, _ctx_env(PRISKV_CRC_STRIDE_G=G, PRISKV_CRC_STRIDE_PRIO=0, **hs))  # two 8-wave workgroups
     per = 64 // G
     rng = np.random.default_rng(G)
     try:
@@ -1426,9 +1429,8 @@ def test_stride_kernel_every_g_and_shape(torch_cuda, G):
                 for sh, c in enumerate(ctxs):
                     plan = c.blocks_plan(view.data_ptr(), nb, bs)
                     # a few unbalanced blocks >= 64 KiB are cut into segments by the fused
-                    # kernel; odd sizes / bases from 4.5 KiB (others from 9 KiB) take the extents kernel
-                    odd = ((bs | mis) & 3) != 0
-                    odd_big = bs >= (4608 if odd else 9216) and c is not ctxs[-1]
+                    # kernel; sizes from 9 KiB take the extents kernel
+                    odd_big = bs >= 9216 and c is not ctxs[-1]
                     assert plan.startswith(f"crc_stride_kernel<G={G},") or (
                         bs >= 65536 and plan.startswith("crc_ranges_fused_kernel")) or (
                         odd_big and plan.startswith("crc_ranges_kernel")), plan
@@ -1494,7 +1496,8 @@ def test_stride_kernel_beyond_4GiB(torch_cuda, ctx):
                                                      ((5 << 20) + 7, 400, 2, "crc_ranges_kernel (extents)", True,
                                                       False),
                                                      (4607, 6000, 1, "crc_stride_kernel<G=32,", False, False),
-                                                     (4609, 6000, 0, "crc_ranges_kernel (extents)", False, False),
+                                                     (4609, 6000, 0, "crc_stride_kernel<G=32,", False, False),
+                                                     (9217, 3000, 0, "crc_ranges_kernel (extents)", False, False),
                                                      (16460, 3000, 0, "crc_ranges_kernel (extents)", False, False),
                                                      (16388, 3000, 0, "crc_rows_kernel<G=64,", False, False),
                                                      (4100, 2049, 4, "crc_rows_kernel<G=64,", False, False)])
@@ -1502,8 +1505,8 @@ def test_stride_kernel_large_and_limit_blocks(torch_cuda, ctx, ctx_noseg, bs, nb
     """Blocks at both sides of the stride kernel's limits: 64 MiB (a few such
     blocks are cut into segments by the fused kernel, or with segmentation
     off and the size limit raised hashed whole by the stride kernel: 65 536
-    rows of 1 KiB; more than 64 MiB keeps the extents path), 4.5 KiB for odd
-    sizes and 9 KiB for multiples of 4 (the extents kernel from there), 2 GB
+    rows of 1 KiB; more than 64 MiB keeps the extents path), 9 KiB (the
+    extents kernel from there), 2 GB
     batches of 5 MiB + 8 / + 7 B blocks, a batch whose last lane-group runs
     are short, and sizes of whole KiB rows + a 4-B head, which the head split
     hands to the rows kernel: the oracle's CRCs."""

@@ -240,8 +240,9 @@ def test_path_selection():
     assert C.blocks_path(4097, 10, 256) == "stride"     # sub-KiB power of two, unaligned base
     # the default limits hand larger stride sizes to the extents kernel
     assert C.blocks_path(4096, 10, 4607) == "stride"
-    assert C.blocks_path(4096, 10, 4609) == "extents"   # odd from 4.5 KiB
-    assert C.blocks_path(4097, 10, 8192) == "extents"   # unaligned base counts as odd
+    assert C.blocks_path(4096, 10, 4609) == "stride"
+    assert C.blocks_path(4096, 10, 9217) == "extents"   # odd from 9 KiB
+    assert C.blocks_path(4097, 10, 9216) == "extents"   # unaligned base counts as odd
     assert C.blocks_path(4096, 10, 9212) == "stride"
     assert C.blocks_path(4096, 10, 9300) == "extents"   # multiples of 4 from 9 KiB (head 84 B)
     assert C.blocks_path(4096, 10, (64 << 20) + 5) == "extents"

@@ -67,6 +67,9 @@ def main():
         ctxs = {"default": ctxs["stride"]}
         for g in (16, 32, 64):
             ctxs[f"G{g}"] = ctx_env(PRISKV_CRC_STRIDE_G=g)
+    elif which in ("prio", "priorefine"):  # round 3: one 16-wave workgroup with progress priority (default) against two 8-wave
+        ctxs = {"default": ctxs["stride"], "noprio": ctx_env(PRISKV_CRC_STRIDE_PRIO=0),
+                "stride_big": ctx_env(PRISKV_CRC_STRIDE_MAX_KIB=1024)}
     elif which == "funnel":
         ctxs["nofunnel"] = ctx_env(PRISKV_CRC_STRIDE_FUNNEL=0)
     elif which == "runs":
@@ -99,6 +102,12 @@ def main():
         if which == "retune":
             cases = [(100, 0), (520, 0), (1000, 0), (3000, 0), (4100, 0), (4096, 4), (4097, 0), (100000, 0),
                      (19, 3), (256, 3)]
+        if which == "prio":
+            cases = [(19, 3), (100, 0), (200, 0), (520, 0), (1000, 0), (3000, 0), (4097, 0), (4096, 1), (4609, 0),
+                     (6145, 0), (8193, 0), (9212, 0), (12289, 0), (12292, 0), (16385, 0), (24580, 0), (65537, 0)]
+        if which == "priorefine":  # the stride / extents crossover with the prioritised stride kernel
+            cases = [(8705, 0), (9217, 0), (9729, 0), (10241, 0), (10753, 0), (11265, 0), (10000, 0), (11000, 0),
+                     (12000, 0), (14000, 0)]
         if which == "oddlarge":  # odd sizes of 8 KiB-256 KiB: stride (funnel) against the extents kernel
             cases = [(8193, 0), (16385, 0), (32769, 0), (65537, 0), (131073, 0), (262145, 0), (16384, 1), (65536, 3)]
         for bs, mis in cases:
