@@ -423,9 +423,13 @@ struct Plan {
 // (profiles/r02/explore_r2e_explore_4k_sweep_{a,b}.log, explore_r2f_4k_{a,b}.log).
 // NBUF3 loses 1-3 % at 8 KiB-1 MiB (profiles/r02/explore_r2f_{8k,64k,1m}.log),
 // so those keep NBUF2.
-constexpr int kPrio1 = 1 << 8, kPrio3 = 3 << 8;
+// Round 3: the 4 KiB plan requests its first chunks before it loads the LDS
+// tables (OPT bit 4): 256 MiB calls 48.4 -> 45.6 us, 64 MiB 16.3 -> 16.1,
+// 4 GiB level (0.2 %); the 64 KiB plan gained nothing and lost 4 % on
+// segmented 64 MiB calls (profiles/r03/early/).
+constexpr int kPrio1 = 1 << 8, kPrio3 = 3 << 8, kEarly = 16;
 constexpr Plan kPlans[NPLANS] = {
-    {64, 4, 3, 2 | 32 | kPrio3, 1, 31, 29}, {64, 4, 2, 32 | kPrio1, 1, 31, 29}, {16, 4, 2, 2 | 32 | kPrio1, 1, 31, 29},
+    {64, 4, 3, 2 | kEarly | 32 | kPrio3, 1, 31, 29}, {64, 4, 2, 32 | kPrio1, 1, 31, 29}, {16, 4, 2, 2 | 32 | kPrio1, 1, 31, 29},
     {16, 4, 2, kPrio1, 1, 31, 29},          {64, 4, 2, kPrio1, 1, 31, 29},      {64, 4, 2, kPrio3, 1, 31, 29},
     {64, 2, 2, 0, 1, 31, 29},               {64, 1, 2, 0, 1, 31, 29}};
 
@@ -766,10 +770,12 @@ int launch_head_split(const priskv_crc_ctx *ctx, const uint8_t *base, uint64_t n
     return herr(hipGetLastError());
 }
 
-// sub-KiB kernel for G = 1 << gl: bit-matrix fold at G = 1; for G >= 2 the
-// nibble fold, with prio in one 16-wave workgroup per CU and progress-priority
-// mode 1 (+0.2-2.6 % at 32-512 B, profiles/r01/prio/small_*.log), else in two
-// 8-wave workgroups per CU (PRISKV_CRC_PRIO=0)
+// sub-KiB kernel for G = 1 << gl: no fold at G = 1 (a lane holds a whole
+// block); G = 2-16 the byte-table fold, G = 32 the nibble fold; with prio in
+// one 16-wave workgroup per CU and progress-priority mode 1 (+0.2-2.6 % at
+// 32-512 B, profiles/r01/prio/small_*.log; round 3 +5 % at 16 B,
+// profiles/r03/bytefold/), else in two 8-wave workgroups per CU
+// (PRISKV_CRC_PRIO=0)
 constexpr int kSmallOptPrio = 1 | (1 << 8) | 1024;
 
 // Chunk shape: 4 rows per chunk with 3 chunks in the register pipeline
@@ -783,8 +789,8 @@ constexpr int kSmallCh = 4, kSmallNbuf = 3, kSmallCh1 = 4, kSmallNbuf1 = 3;
 template <int G>
 const void *small_fn_g(bool prio, bool bf)
 {
-    if (bf && G <= 16)
-        return prio ? reinterpret_cast<const void *>(&crc_small_kernel<G, kSmallOptPrio | 2, kSmallCh, kSmallNbuf>)
+    if (bf && G <= 16) // first chunks before the tables (OPT bit 2): 256 MiB calls -2.5-3 %, 4 GiB level
+        return prio ? reinterpret_cast<const void *>(&crc_small_kernel<G, kSmallOptPrio | 2 | 4, kSmallCh, kSmallNbuf>)
                     : reinterpret_cast<const void *>(&crc_small_kernel<G, 3>);
     return prio ? reinterpret_cast<const void *>(&crc_small_kernel<G, kSmallOptPrio, kSmallCh, kSmallNbuf>)
                 : reinterpret_cast<const void *>(&crc_small_kernel<G, 1>);
@@ -793,7 +799,8 @@ const void *small_fn_g(bool prio, bool bf)
 const void *small_fn(int gl, bool prio, bool bf)
 {
     switch (gl) {
-    case 0: return reinterpret_cast<const void *>(&crc_small_kernel<1, 0, kSmallCh1, kSmallNbuf1>);
+    case 0: return prio ? reinterpret_cast<const void *>(&crc_small_kernel<1, kSmallOptPrio, kSmallCh1, kSmallNbuf1>)
+                        : reinterpret_cast<const void *>(&crc_small_kernel<1, 0, kSmallCh1, kSmallNbuf1>);
     case 1: return small_fn_g<2>(prio, bf);
     case 2: return small_fn_g<4>(prio, bf);
     case 3: return small_fn_g<8>(prio, bf);
@@ -900,10 +907,13 @@ const void *stride_fn_g(int shape, bool odd, bool bf, int prio)
     constexpr bool small = G < 16;
     // one 16-wave workgroup per CU with progress-priority mode 3 (default
     // shape; G <= 8 with the byte fold)
+    // G >= 16 with aligned loads requests its first chunks before the tables
+    // (256 MiB of 1000-B blocks -2-5 %; the funnel-shift variant lost 5 % at
+    // 4097 B and G <= 8 was level: profiles/r03/early/)
     if constexpr (G >= 16) {
         if (prio && shape == 0)
             return odd ? reinterpret_cast<const void *>(&crc_stride_kernel<G, 8, 2, kAux, true, false, 3>)
-                       : reinterpret_cast<const void *>(&crc_stride_kernel<G, 8, 2, kAux, false, false, 3>);
+                       : reinterpret_cast<const void *>(&crc_stride_kernel<G, 8, 2, kAux, false, false, 3, true>);
     } else {
         if (prio && bf && shape == 0)
             return odd ? reinterpret_cast<const void *>(&crc_stride_kernel<G, 8, 2, kAux, true, true, 3>)
@@ -1019,7 +1029,7 @@ int launch_blocks(const priskv_crc_ctx *ctx, const uint8_t *base, uint64_t nbloc
             const bool bf = ctx->small_bf && gl >= 1 && gl <= 4;
             const uint32_t *fold = gl ? ctx->d_nibrep[gl] : ctx->d_fold;
             const uint32_t *img = bf ? ctx->d_small_img[gl] : ctx->d_lds_image[0];
-            const bool prio = gl && ctx->prio;
+            const bool prio = ctx->prio;
             const int waves = prio ? 2 * kWaves : kWaves;
             const uint64_t cap = prio ? (uint64_t)ctx->num_cus : (uint64_t)ctx->max_wgs;
             const uint64_t chw = (uint64_t)(gl == 0 ? kSmallCh1 : prio ? kSmallCh : 4) * waves; // rows per wave-chunk

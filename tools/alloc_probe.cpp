@@ -86,7 +86,9 @@ __global__ __launch_bounds__(64 * NW, 1) void read_roof_buf(const uint8_t *__res
 int main(int argc, char **argv)
 {
     const int K = argc > 1 ? atoi(argv[1]) : 4;
-    const uint64_t bytes = (argc > 2 ? strtoull(argv[2], 0, 0) : 4) << 30;
+    // ALLOC_PROBE_MIB=M: regions of M MiB instead of GiB
+    const uint64_t bytes = getenv("ALLOC_PROBE_MIB") ? strtoull(getenv("ALLOC_PROBE_MIB"), 0, 0) << 20
+                                                     : (argc > 2 ? strtoull(argv[2], 0, 0) : 4) << 30;
     const int rounds = argc > 3 ? atoi(argv[3]) : 3;
     const uint64_t pad = (argc > 4 ? strtoull(argv[4], 0, 0) : 0) << 20;
     std::vector<uint32_t> sizes;
