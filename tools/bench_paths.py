@@ -262,6 +262,11 @@ def main():
         ranges_dev_case(ctx)
         ranges_dev_case(ctx, bs=65536, n=1 << 15)
         ranges_dev_case(ctx, bs=1 << 20, n=1 << 11)
+    if "host" in which:
+        ranges_host_case(ctx)
+        blocks_host_case(ctx)
+    if "memfile" in which:
+        memfile_case(ctx)
     if "few" in which or "ranges" in which:
         os.environ["PRISKV_CRC_SEGMENT"] = "0"
         ctx_noseg = CrcContext(0)
