@@ -905,11 +905,11 @@ template <int G>
 const void *stride_fn_g(int shape, bool odd, bool bf, int prio)
 {
     constexpr bool small = G < 16;
-    // one 16-wave workgroup per CU with progress-priority mode 3 (default
-    // shape; G <= 8 with the byte fold)
-    // G >= 16 with aligned loads requests its first chunks before the tables
-    // (256 MiB of 1000-B blocks -2-5 %; the funnel-shift variant lost 5 % at
-    // 4097 B and G <= 8 was level: profiles/r03/early/)
+    // One 16-wave workgroup per CU with progress-priority mode 3 (default
+    // shape; G <= 8 only with the byte fold).  G >= 16 with aligned loads
+    // also requests its first chunks before the tables (256 MiB of 1000-B
+    // blocks -2-5 %; the funnel-shift variant lost 5 % at 4097 B and G <= 8
+    // was level: profiles/r03/early/).
     if constexpr (G >= 16) {
         if (prio && shape == 0)
             return odd ? reinterpret_cast<const void *>(&crc_stride_kernel<G, 8, 2, kAux, true, false, 3>)
