@@ -6,7 +6,7 @@
 // times priskv_crc32_blocks_dev over every region for every block size in
 // turn, R rounds round-robin, and prints one JSON line per (region, size)
 // with the region's virtual address and its alignment.  ALLOC_PROBE_ENV2=
-// "VAR=V[:VAR=V]" adds a second context created with those variables set,
+// "VAR=V[;VAR=V]" adds a second context created with those variables set,
 // timed right after the first on every (region, size): an A/B that holds
 // the allocation fixed.
 // Usage: alloc_probe [K=4] [GiB=4] [rounds=3] [pad_MiB=0] [bs,bs,...=256,4096]
@@ -107,7 +107,7 @@ int main(int argc, char **argv)
         char buf[512];
         snprintf(buf, sizeof(buf), "%s", e2);
         std::vector<std::string> names;
-        for (char *t = strtok(buf, ":"); t; t = strtok(nullptr, ":")) {
+        for (char *t = strtok(buf, ";"); t; t = strtok(nullptr, ";")) {
             char *eq = strchr(t, '=');
             if (!eq)
                 continue;
