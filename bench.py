@@ -70,6 +70,7 @@ RAMP_MIN_S = 1.0
 RAMP_MAX_S = 4.0
 COLD_IDLE_S = 1.0
 EXIT_DEVICES = 3
+T_START = time.perf_counter()  # reset at main(); leg_wall_s counts from it
 
 CONFIGS = {
     # name: (block_size, nblocks per GPU, description)
@@ -193,6 +194,57 @@ def ramp(fn, stream, torch, window=16, min_s=RAMP_MIN_S, max_s=RAMP_MAX_S):
         prev = cur
 
 
+def progress(rank, msg):
+    """A progress line on stderr (rank 0): a multi-rank run with slow legs
+    keeps showing signs of life; stdout carries only the JSON line."""
+    if rank == 0:
+        print(f"bench.py: {msg} ({time.perf_counter() - T_START:.1f} s since start)", file=sys.stderr, flush=True)
+
+
+def per_launch_ms(fn, stream, torch, k):
+    """k launches, one event pair around each (a second window after the
+    timed one): per-launch kernel times in ms."""
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(k)]
+    for e0, e1 in evs:
+        e0.record(stream)
+        fn()
+        e1.record(stream)
+    evs[-1][1].synchronize()
+    return [e0.elapsed_time(e1) for e0, e1 in evs]
+
+
+def launch_stats(ms):
+    a = np.asarray(ms, dtype=np.float64)
+    return {"launches": int(a.size), "median_ms": round(float(np.median(a)), 4), "min_ms": round(float(a.min()), 4),
+            "max_ms": round(float(a.max()), 4)}
+
+
+def read_roof(B, region, bs, nb, stream, alg, k):
+    """The measured peak beside the CRC's roofline: priskv_crc_read_roof_dev
+    (the CRC kernel's loads, per-wave ranges, pipeline depth and XCD split,
+    no hashing) over the same region, ramped like the CRC, k launches with
+    one event pair each.  GB/s of the same algorithmic bytes."""
+    torch = B.torch
+    sink = torch.empty(nb, dtype=torch.int32, device=B.dev)
+
+    def step():
+        B.ctx.read_roof_dev(region, bs, sink, stream=stream, nblocks=nb)
+
+    step()
+    torch.cuda.synchronize()
+    ramp(step, stream, torch, window=8, min_s=0.3, max_s=2.0)
+    ms = per_launch_ms(step, stream, torch, k)
+    del sink
+    st = launch_stats(ms)
+    mean = float(np.mean(ms))
+    return {"measured_peak": round(alg / (mean * 1e-3) / 1e9, 1),
+            "measured_peak_best": round(alg / (st["min_ms"] * 1e-3) / 1e9, 1),
+            "measured_peak_source": "priskv_crc_read_roof_dev on the same region in this process: the CRC kernel's "
+                                    "loads, per-wave ranges, pipeline depth and XCD split without hashing; mean of "
+                                    f"{k} launches (one event pair each) after a ramp",
+            "roof_launch_ms": st}
+
+
 class Bench:
     """Per-rank state shared by the legs."""
 
@@ -273,6 +325,9 @@ def resident_leg(B: Bench, name, steps, parity="full"):
     ramp(step, stream, torch, window=max(3, min(16, (64 << 30) // (bs * nb))), min_s=0.5)
     k = max(1, steps)
     el, kms = B.timed(step, stream, k)
+    alg = nb * (bs + 4)
+    lstats = launch_stats(per_launch_ms(step, stream, torch, k))
+    roof = read_roof(B, region, bs, nb, stream, alg, k) if bs % 4096 == 0 else None
     if parity == "full":
         host = region.cpu().numpy()
         got = as_u32(out)
@@ -287,17 +342,19 @@ def resident_leg(B: Bench, name, steps, parity="full"):
         want = O.crc32_blocks(blocks.reshape(-1), bs, nthreads=8)
         nchk, what = int(idx.size), "first, last, every 4096th block"
     ok = B.all_ok(bool(np.array_equal(got, want)))
-    alg = nb * (bs + 4)
     plan = ctx.blocks_plan(region.data_ptr(), nb, bs)
     del region, out
     torch.cuda.empty_cache()
     achieved = alg / (kms * 1e-3) / 1e9
+    rl = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": load_traffic(bs, nb), "kernel_ms": round(kms, 4),
+          "alg_bytes_per_launch": alg, "kernel_launch_ms": lstats}
+    if roof:
+        rl.update(roof)
+        rl["frac_of_measured"] = round(achieved / roof["measured_peak"], 4)
     return {"workload": desc, "value": round(bs * nb * B.world * k / el / 2**30, 2), "unit": "GiB/s",
             "n_gpus": B.world, "steps": k, "ms_per_step": round(el / k * 1e3, 4), "bytes_per_gpu": bs * nb,
-            "kernel": plan,
-            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4), "kernel_ms": round(kms, 4),
-                         "alg_bytes_per_launch": alg},
+            "kernel": plan, "roofline": rl,
             "parity": {"checked_blocks_per_rank": nchk, "sample": what, "bit_exact": ok,
                        "oracle": "oracle/crc_oracle.c"}}
 
@@ -414,6 +471,8 @@ def cpu_model():
 
 
 def main():
+    global T_START
+    T_START = time.perf_counter()
     args = parse()
     import torch
     import torch.distributed as dist
@@ -459,6 +518,8 @@ def main():
         bs = args.block_size
     if args.nblocks:
         nb = args.nblocks
+    walls = {"start_to_context": time.perf_counter() - T_START}
+    t_leg = time.perf_counter()
     ctx = CrcContext(gpu)
     B = Bench(args, torch, dist, world, rank, dev, ctx)
     # weak scaling: the global region has world * nb blocks; this rank's shard
@@ -475,16 +536,26 @@ def main():
     def step():
         ctx.blocks_dev(region, bs, out=out, stream=stream)
 
+    walls["setup"] = time.perf_counter() - t_leg
+    t_leg = time.perf_counter()
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
     nramp, ramp_s = ramp(step, stream, torch)
 
     elapsed_max, kernel_ms = B.timed(step, stream, args.steps)
+    walls["headline"] = time.perf_counter() - t_leg
+
+    # a second window, one event pair per launch (median / min), then the
+    # read roof of the same access pattern over the same region
+    t_leg = time.perf_counter()
+    alg_bytes = nb * (bs + 4)  # block read + 4-byte CRC written (SURVEY §8d)
+    lstats = launch_stats(per_launch_ms(step, stream, torch, args.steps))
+    roof = read_roof(B, region, bs, nb, stream, alg_bytes, args.steps) if bs % 4096 == 0 else None
+    walls["launch_stats_and_roof"] = time.perf_counter() - t_leg
 
     total_bytes = bs * nb * world
     value = total_bytes * args.steps / elapsed_max / 2**30
-    alg_bytes = nb * (bs + 4)  # block read + 4-byte CRC written (SURVEY §8d)
     achieved = alg_bytes / (kernel_ms * 1e-3) / 1e9
     traffic = load_traffic(bs, nb)
     path = ctx.blocks_plan(region.data_ptr(), nb, bs)  # the library reports its own plan
@@ -510,46 +581,58 @@ def main():
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": traffic, "kernel_ms": round(kernel_ms, 4),
-                     "alg_bytes_per_launch": alg_bytes},
+                     "alg_bytes_per_launch": alg_bytes, "kernel_launch_ms": lstats},
     }
+    if roof:
+        result["roofline"].update(roof)
+        result["roofline"]["frac_of_measured"] = round(achieved / roof["measured_peak"], 4)
 
     # the whole shard to host (untimed): every block is checked against the
     # oracle, rank 0's first cpu-sample-bytes time the CPU baseline, and the
     # streamed leg reads these same bytes from host memory
+    t_leg = time.perf_counter()
     host = region.cpu().numpy()
     gpu_crc = as_u32(out)
     want = O.crc32_blocks(host, bs, nthreads=8)
     head_ok = B.all_ok(bool(np.array_equal(gpu_crc, want)))
+    walls["parity"] = time.perf_counter() - t_leg
+    progress(rank, f"headline {value:.1f} GiB/s, parity {'ok' if head_ok else 'FAILED'}")
     walked = region if args.config == "default" else None
     if walked is None:
         del region
     del out
     torch.cuda.empty_cache()
 
-    def leg(fn, *a, **kw):
-        """A leg beside the headline.  On one rank a failure is reported in
-        the line instead of losing the headline; with several ranks it
-        propagates (its collectives could no longer pair up)."""
-        if world > 1:
-            return fn(*a, **kw)
+    def leg(label, fn, *a, **kw):
+        """A leg beside the headline, its wall time recorded under `label`.
+        On one rank a failure is reported in the line instead of losing the
+        headline; with several ranks it propagates (its collectives could no
+        longer pair up)."""
+        t0 = time.perf_counter()
         try:
-            return fn(*a, **kw)
-        except Exception as e:  # noqa: BLE001 -- reported in the line
-            torch.cuda.synchronize()
-            torch.cuda.empty_cache()
-            return {"error": f"{type(e).__name__}: {e}"}
+            if world > 1:
+                return fn(*a, **kw)
+            try:
+                return fn(*a, **kw)
+            except Exception as e:  # noqa: BLE001 -- reported in the line
+                torch.cuda.synchronize()
+                torch.cuda.empty_cache()
+                return {"error": f"{type(e).__name__}: {e}"}
+        finally:
+            walls[label] = time.perf_counter() - t0
+            progress(rank, f"{label} done in {walls[label]:.1f} s")
 
     if not args.no_sweep and args.config == "default":
-        result["sweep"] = {k: leg(resident_leg, B, name, args.sweep_steps) for k, name in SWEEP}
+        result["sweep"] = {k: leg(f"sweep_{k}", resident_leg, B, name, args.sweep_steps) for k, name in SWEEP}
     if not args.no_tib and args.config == "default":
-        result["tib"] = leg(resident_leg, B, "tib", args.tib_steps, parity="sampled")
+        result["tib"] = leg("tib", resident_leg, B, "tib", args.tib_steps, parity="sampled")
     if not args.no_streamed:
-        result["streamed"] = leg(streamed_leg, B, host, bs, want)
+        result["streamed"] = leg("streamed", streamed_leg, B, host, bs, want)
     # cold passes LAST on the GPU: what a one-off recovery scrub sees (clock
     # ramp included); measured last so that the idle cannot leave its slower
     # first launches inside the other legs
     if walked is not None:
-        result["cold"] = leg(cold_leg, B, bs, nb, walked)
+        result["cold"] = leg("cold", cold_leg, B, bs, nb, walked)
         if "ms" in result["cold"]:
             result["cold_ms"] = result["cold"]["ms"]
         del walked
@@ -563,11 +646,19 @@ def main():
     result["parity"] = {"checked_blocks_per_rank": nb, "sample": "every block", "bit_exact": head_ok,
                         "oracle": "oracle/crc_oracle.c"}
     if rank == 0 and not args.no_cpu_baseline:
+        t_leg = time.perf_counter()
         nsamp = max(1, min(nb, args.cpu_sample_bytes // bs))
         result["cpu_baseline"], cpu_ok = cpu_baseline(O, host[: nsamp * bs], bs, gpu_crc[:nsamp])
         result["parity"]["bit_exact_vs_reference_build"] = cpu_ok
+        walls["cpu_baseline"] = time.perf_counter() - t_leg
+    t_leg = time.perf_counter()
     B.barrier()
+    walls["final_barrier"] = time.perf_counter() - t_leg
+    walls["total"] = time.perf_counter() - T_START
     if rank == 0:
+        result["leg_wall_s"] = {k: round(v, 2) for k, v in walls.items()}
+        result["leg_wall_s"]["note"] = ("rank 0's wall seconds per leg (process start to the line); the legs "
+                                        "open and close with barriers, so rank 0's time is the job's")
         print(json.dumps(result), flush=True)
     if world > 1:
         dist.destroy_process_group()

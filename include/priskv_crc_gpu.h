@@ -201,6 +201,18 @@ int priskv_crc32_blocks_path(const void *d_base, uint64_t nblocks, uint32_t bloc
 int priskv_crc32_blocks_plan(const priskv_crc_ctx *ctx, const void *d_base, uint64_t nblocks, uint32_t block_size,
                              char *buf, uint64_t len);
 
+/* Diagnostic: the read roof of the CRC kernel's access pattern.  Reads
+ * nblocks x block_size bytes at d_base with exactly the loads, per-wave
+ * ranges, pipeline depth and XCD split crc_rows_kernel uses for this block
+ * size (block_size a multiple of 4 KiB, d_base 16-byte aligned), without
+ * hashing, and stores one word per wave into d_sink (nblocks uint32 entries;
+ * which entries are written is unspecified).  Timing it beside
+ * priskv_crc32_blocks_dev on the same region gives the fraction of what HBM
+ * delivers for this pattern that the CRC reaches.  Asynchronous on stream;
+ * 0 or -EINVAL / -ENODEV / -EIO. */
+int priskv_crc_read_roof_dev(const priskv_crc_ctx *ctx, const void *d_base, uint64_t nblocks,
+                             uint32_t block_size, uint32_t *d_sink, void *stream);
+
 const char *priskv_crc_version(void);
 
 #if defined(__cplusplus)

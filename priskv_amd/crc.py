@@ -69,6 +69,8 @@ SIGNATURES = [
     ("priskv_crc32_blocks_path", _C.c_int, [_C.c_void_p, _C.c_uint64, _C.c_uint32]),
     ("priskv_crc32_blocks_plan", _C.c_int,
      [_C.c_void_p, _C.c_void_p, _C.c_uint64, _C.c_uint32, _C.c_char_p, _C.c_uint64]),
+    ("priskv_crc_read_roof_dev", _C.c_int,
+     [_C.c_void_p, _C.c_void_p, _C.c_uint64, _C.c_uint32, _C.c_void_p, _C.c_void_p]),
     ("priskv_crc_version", _C.c_char_p, []),
 ]
 
@@ -264,6 +266,17 @@ class CrcContext:
         _check(lib().priskv_crc_fill_splitmix_dev(self._h, region.data_ptr(), nb, seed & (2**64 - 1),
                                                   word_offset, _stream_ptr(stream)),
                "priskv_crc_fill_splitmix_dev")
+
+    def read_roof_dev(self, region, block_size: int, sink, stream=None, nblocks: Optional[int] = None) -> None:
+        """Diagnostic read roof of the CRC kernel's access pattern over `region`
+        (priskv_crc_read_roof_dev; sink: >= nblocks 4-byte entries)."""
+        nbytes = region.numel() * region.element_size()
+        n = nbytes // block_size if nblocks is None else nblocks
+        if n * block_size > nbytes or sink.numel() < n or sink.element_size() != 4 or not sink.is_contiguous():
+            raise ValueError("nblocks * block_size must fit the region and sink hold >= nblocks 4-byte entries")
+        _device_args(region, sink)
+        _check(lib().priskv_crc_read_roof_dev(self._h, region.data_ptr(), n, block_size, sink.data_ptr(),
+                                              _stream_ptr(stream)), "priskv_crc_read_roof_dev")
 
     # ---- host-resident (streamed over PCIe)
     def blocks_host(self, region: np.ndarray, block_size: int, out: Optional[np.ndarray] = None) -> np.ndarray:

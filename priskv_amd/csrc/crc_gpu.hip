@@ -73,7 +73,6 @@ struct priskv_crc_ctx {
     int balance;               // byte-balanced extents split (PRISKV_CRC_BALANCE=0: off)
     int ext_adapt;             // per-wave chunk size of the many-extents shape (PRISKV_CRC_EXT_ADAPT=0: 2 rows)
     int head_split;            // rows kernel + head terms for B = h + whole KiB rows (PRISKV_CRC_HEADSPLIT=0: off)
-    int fused_ch;              // rows per chunk of the fused few-extents kernel (PRISKV_CRC_FUSED_CH=2/4/8; tuning)
     uint64_t seg_max_extents;  // device-resident lengths: segment calls of at most this many extents
     int xcd_rr;                // the XCD probe found workgroup b on XCD b % 8 (weights apply)
     uint64_t tile_min_bytes;   // rows batches of at least this many bytes run in block-cyclic tiles
@@ -84,7 +83,7 @@ struct priskv_crc_ctx {
     uint32_t *d_nib16;         // the extents kernel's: G = 16, width 16 (8 KiB)
     uint32_t *d_small_img[5];  // sub-KiB byte-fold images for G = 1 << j, j = 1..4 (prv_small_image)
     int small_bf;              // sub-KiB kernel folds through byte tables (PRISKV_CRC_SMALL_BF=0: nibble tables)
-    int stride_prio;           // stride kernel (G >= 16): progress-priority mode in one 16-wave workgroup per CU
+    int stride_prio;           // stride kernel: progress-priority mode in one 16-wave workgroup per CU (0 with PRIO=0)
     uint32_t *d_sarwate;       // 256 words
     uint32_t *d_zpow;          // kZpowRows x 32 words: columns of Z_(2^k) (segment combine)
     uint32_t *d_rowshift;      // 16 x 4 x 32 words: columns of Z_-p o Z_(256(3-k)) (extents fold)
@@ -111,13 +110,9 @@ struct priskv_crc_ctx {
     int fused;                 // few extents in one launch (PRISKV_CRC_FUSED=0: the three-launch path)
     int stride;                // odd block sizes / unaligned bases take crc_stride_kernel (PRISKV_CRC_STRIDE=0: the
                                // extents / generic kernels, as in round 2)
-    int stride_g;              // PRISKV_CRC_STRIDE_G: force the stride kernel's G (0 = cost model; tuning)
-    int stride_shape;          // PRISKV_CRC_STRIDE_SHAPE: chunk shape variant (tuning)
-    int stride_wgs;            // PRISKV_CRC_STRIDE_WGS=1: one workgroup per CU instead of two (tuning)
-    int stride_funnel;         // PRISKV_CRC_STRIDE_FUNNEL=0: odd sizes / bases load unaligned (tuning)
-    int stride_runs;           // PRISKV_CRC_STRIDE_RUNS=1: G >= 16 lane groups in runs, not side by side (tuning)
+    int stride_g;              // PRISKV_CRC_STRIDE_G: force the stride kernel's G (0 = cost model; tests)
     uint64_t stride_max;       // blocks from this size (multiples of 4) take the extents path,
-    uint64_t stride_odd_max;   // and odd ones from this (PRISKV_CRC_STRIDE_MAX_KIB sets both; tuning, tests)
+    uint64_t stride_odd_max;   // and odd ones from this (PRISKV_CRC_STRIDE_MAX_KIB sets both; tests)
 };
 
 namespace {
@@ -589,7 +584,6 @@ constexpr uint32_t kSegMinLen = 64u << 10;
 // progress priority off in the fused kernel: 1 x 256 MiB 49.7 us vs 50.7 with
 // mode 3, 4096 small values 7.6 vs 7.7 us (profiles/r02/fused/ktrace_shapes_*)
 constexpr int kFusedPrio = 0;
-constexpr int kFusedCh = 2; // rows per chunk (PRISKV_CRC_FUSED_CH)
 
 // one segment size per call (crc_seg_plan_kernel / the fused kernel): about
 // kSegPerWave full segments per resident wave, so the count split of
@@ -630,12 +624,9 @@ int launch_fused(const priskv_crc_ctx *ctx, const uint8_t *base, uint64_t n, con
     const uint8_t *abase = base - sh;
     const uint32_t *lens_or_null = offs ? lens : nullptr;
     const uint32_t tgt = 1u << (31 - __builtin_clz((uint32_t)seg_target(ctx))); // the kernel takes a power of two
-    const void *fn = ctx->fused_ch == 8 ? reinterpret_cast<const void *>(
-                                              &crc_ranges_fused_kernel<8, kNbuf, kAux, kFusedPrio, kFusedWaves>)
-                     : ctx->fused_ch == 4 ? reinterpret_cast<const void *>(
-                                              &crc_ranges_fused_kernel<4, kNbuf, kAux, kFusedPrio, kFusedWaves>)
-                                          : reinterpret_cast<const void *>(
-                                              &crc_ranges_fused_kernel<kExtRows, kNbuf, kAux, kFusedPrio, kFusedWaves>);
+    // 2-row chunks: 4 and 8 rows lost 6-13 % on a lone 256 MiB value (profiles/r03/fused/)
+    const void *fn =
+        reinterpret_cast<const void *>(&crc_ranges_fused_kernel<kExtRows, kNbuf, kAux, kFusedPrio, kFusedWaves>);
     const uint32_t *img = ctx->d_lds_image[0], *nib = ctx->d_nib16, *rs = ctx->d_rowshift, *zp = ctx->d_zpow;
     uint32_t ms = kSegMinShift;
     void *args[] = {(void *)&abase, (void *)&n,   (void *)&offs, (void *)&lens_or_null, (void *)&sh,
@@ -746,14 +737,24 @@ int launch_rows_plain(const priskv_crc_ctx *ctx, const uint8_t *base, uint64_t n
 // (stride B, 4-byte aligned loads stream at full rate) and crc_head_kernel
 // adds each head's term Z_body(crc(head)).  A 4096-B value with a 4-B
 // trailer, 4100 B, thus runs on the 4 KiB plan instead of the stride
-// kernel's 9 rows of 512 B for 4100 (12 % of them padding).  Batches that
-// would need segmenting (few large blocks) keep the stride / extents paths.
-// PRISKV_CRC_HEADSPLIT=0 turns it off.
+// kernel's 9 rows of 512 B for 4100 (12 % of them padding).  The bodies run
+// unsegmented, so a batch of few large blocks -- one the extents path would
+// segment: bodies of at least kSegMinLen and a count split that is not
+// balanced over the rows kernel's waves -- keeps the stride / extents paths,
+// which hand it to the fused kernel (whatever the body: 1023 KiB bodies cannot
+// be halved into whole-KiB segments, and one wave streams ~3.4 GB/s).
+// PRISKV_CRC_HEADSPLIT=0 turns it off.  ctx = nullptr: a default context on
+// a device of kNominalCus CUs (priskv_crc32_blocks_path).
+constexpr int kNominalCus = 256; // MI355X
 bool head_split(const priskv_crc_ctx *ctx, const void *base, uint64_t nblocks, uint32_t bs)
 {
-    const uint32_t h = bs % PRV_ROW_BYTES;
-    return (!ctx || ctx->head_split) && bs % 4 == 0 && ((uintptr_t)base & 3) == 0 && h >= 4 && h <= kHeadMax &&
-           bs - h >= PRV_ROW_BYTES && (!ctx || segments_for(ctx, nblocks, bs - h) == 1);
+    const uint32_t h = bs % PRV_ROW_BYTES, body = bs - h;
+    if (!((!ctx || ctx->head_split) && bs % 4 == 0 && ((uintptr_t)base & 3) == 0 && h >= 4 && h <= kHeadMax &&
+          body >= PRV_ROW_BYTES))
+        return false;
+    const bool seg = ctx ? ctx->segment != 0 : true;
+    const uint64_t waves = (uint64_t)(ctx ? ctx->num_cus : kNominalCus) * kWaves;
+    return !seg || body < kSegMinLen || balanced(nblocks, waves);
 }
 
 int launch_head_split(const priskv_crc_ctx *ctx, const uint8_t *base, uint64_t nblocks, uint32_t bs, uint32_t *out,
@@ -789,12 +790,19 @@ constexpr int kSmallCh = 4, kSmallNbuf = 3, kSmallCh1 = 4, kSmallNbuf1 = 3;
 template <int G>
 const void *small_fn_g(bool prio, bool bf)
 {
-    if (bf && G <= 16) // first chunks before the tables (OPT bit 2): 256 MiB calls -2.5-3 %, 4 GiB level
-        return prio ? reinterpret_cast<const void *>(&crc_small_kernel<G, kSmallOptPrio | 2 | 4, kSmallCh, kSmallNbuf>)
-                    : reinterpret_cast<const void *>(&crc_small_kernel<G, 3>);
+    if constexpr (G <= 8) // without priority (two 8-wave workgroups per CU): the 64 KiB byte-fold image
+        if (bf && !prio)
+            return reinterpret_cast<const void *>(&crc_small_kernel<G, 3>);
+    if (bf && prio && G <= 16) // first chunks before the tables (OPT bit 2): 256 MiB calls -2.5-3 %, 4 GiB level
+        return reinterpret_cast<const void *>(&crc_small_kernel<G, kSmallOptPrio | 2 | 4, kSmallCh, kSmallNbuf>);
     return prio ? reinterpret_cast<const void *>(&crc_small_kernel<G, kSmallOptPrio, kSmallCh, kSmallNbuf>)
                 : reinterpret_cast<const void *>(&crc_small_kernel<G, 1>);
 }
+
+// byte fold for G = 2..8; for G = 16 only with progress priority: its 128 KiB
+// image leaves room for one workgroup per CU, which the 16-wave priority
+// shape fills and two 8-wave workgroups would not
+bool small_bf(const priskv_crc_ctx *ctx, int gl) { return ctx->small_bf && gl >= 1 && gl <= (ctx->prio ? 4 : 3); }
 
 const void *small_fn(int gl, bool prio, bool bf)
 {
@@ -835,21 +843,23 @@ constexpr uint32_t kStrideMaxBlock = 64u << 20; // larger odd blocks keep the (s
 // Round 3: with progress priority in one 16-wave workgroup the stride kernel
 // leads odd sizes up to 8.5 KiB (4609 B 5.84 / 5.19 extents, 8193 B 6.10 /
 // 5.70, 8705 B 6.01 / 5.88) and trails from 9 KiB (9217 B 6.04 / 6.11,
-// 10 241 B 6.01 / 6.37; profiles/r03/stride_prio/), so both limits are 9 KiB.
-// PRISKV_CRC_STRIDE_MAX_KIB sets both (tuning, and the tests of the
-// kernel's large-block limits).
+// 10 241 B 6.01 / 6.37; profiles/r03/stride_prio/), so both limits are 9 KiB
+// -- with progress priority.  Without it (PRISKV_CRC_PRIO=0) odd blocks keep
+// round 2's 4.5 KiB limit.  PRISKV_CRC_STRIDE_MAX_KIB sets both (the tests
+// of the kernel's large-block limits).
 constexpr uint32_t kStrideOddMax = 9u << 10;
+constexpr uint32_t kStrideOddMaxNoPrio = 4608;
 constexpr uint32_t kStrideMax = 9u << 10;
 
-bool stride_to_extents_lim(const void *base, uint32_t bs, uint64_t odd_max, uint64_t max, bool funnel)
+bool stride_to_extents_lim(const void *base, uint32_t bs, uint64_t odd_max, uint64_t max)
 {
     const bool odd = (((uintptr_t)base | bs) & 3u) != 0;
-    return bs > kStrideMaxBlock || (odd && bs >= odd_max && funnel) || (!odd && bs >= max);
+    return bs > kStrideMaxBlock || (odd && bs >= odd_max) || (!odd && bs >= max);
 }
 
 bool stride_to_extents(const priskv_crc_ctx *ctx, const void *base, uint32_t bs)
 {
-    return stride_to_extents_lim(base, bs, ctx->stride_odd_max, ctx->stride_max, ctx->stride_funnel);
+    return stride_to_extents_lim(base, bs, ctx->stride_odd_max, ctx->stride_max);
 }
 
 // the extents-path kernels a batch of n extents of at most max_len bytes
@@ -885,65 +895,49 @@ StridePlan stride_plan(const priskv_crc_ctx *ctx, uint32_t bs)
     return best;
 }
 
-// workgroups per CU: two when their LDS fits (64 KiB image + the nibble
-// tables, 16 KiB for G <= 32; G = 64 needs 32 KiB), PRISKV_CRC_STRIDE_WGS=1
-// forces one.  Two gain 18-28 % below 1 KiB, 0-12 % from 1000 to 4097 B
-// (profiles/r02/stride/sweep_retune.jsonl, order-rotated).
-int stride_wgs(const priskv_crc_ctx *ctx, int G) { return G <= 32 ? ctx->stride_wgs : 1; }
+// workgroups per CU without progress priority: two 8-wave workgroups when
+// their LDS fits (64 KiB image + the nibble tables, 16 KiB for G <= 32; G =
+// 64 needs 32 KiB).  Two gain 18-28 % below 1 KiB, 0-12 % from 1000 to
+// 4097 B over one (profiles/r02/stride/sweep_retune.jsonl, order-rotated).
+int stride_wgs(int G) { return G <= 32 ? 2 : 1; }
 
-// Chunk shapes (rows per chunk CH x chunks in flight NBUF).  0, the
-// default: 8 x 2, two workgroups per CU (the shapes differed by 2-8 % either
-// way with the context order; profiles/r02/stride/sweep_tune.jsonl).  1-3: tuning
-// variants (PRISKV_CRC_STRIDE_SHAPE): 4 x 3 (4 x 2 for G < 16), 2 x 4, and
-// 4 x 2 (4 x 3 for G < 16), the first version's.
-constexpr int kStrideShape[4][2] = {{8, 2}, {4, 3}, {2, 4}, {4, 2}};
-
-// odd: a block size or base that is not a multiple of 4 -- the default
-// shape has a variant with aligned loads and funnel shifts; the
-// tuning shapes load at the unaligned rate
+// Chunks of 8 rows, 2 in flight (4 x 3, 2 x 4 and 4 x 2 differed by 2-8 %
+// either way with the context order and were dropped: profiles/r02/stride/
+// sweep_tune.jsonl).  odd: a block size or base that is not a multiple of 4
+// -- aligned loads and funnel shifts (unaligned loads stream at
+// 5.3 of 7.0 TB/s).  bf: the byte-table fold (G <= 8).  prio: one 16-wave
+// workgroup per CU with progress-priority mode 3; G >= 16 with aligned loads
+// also requests its first chunks before the tables (256 MiB of 1000-B blocks
+// -2-5 %; the funnel-shift variant lost 5 % at 4097 B and G <= 8 was level:
+// profiles/r03/early/).
 template <int G>
-const void *stride_fn_g(int shape, bool odd, bool bf, int prio)
+const void *stride_fn_g(bool odd, bool bf, int prio)
 {
-    constexpr bool small = G < 16;
-    // One 16-wave workgroup per CU with progress-priority mode 3 (default
-    // shape; G <= 8 only with the byte fold).  G >= 16 with aligned loads
-    // also requests its first chunks before the tables (256 MiB of 1000-B
-    // blocks -2-5 %; the funnel-shift variant lost 5 % at 4097 B and G <= 8
-    // was level: profiles/r03/early/).
     if constexpr (G >= 16) {
-        if (prio && shape == 0)
+        if (prio)
             return odd ? reinterpret_cast<const void *>(&crc_stride_kernel<G, 8, 2, kAux, true, false, 3>)
                        : reinterpret_cast<const void *>(&crc_stride_kernel<G, 8, 2, kAux, false, false, 3, true>);
     } else {
-        if (prio && bf && shape == 0)
+        if (prio && bf)
             return odd ? reinterpret_cast<const void *>(&crc_stride_kernel<G, 8, 2, kAux, true, true, 3>)
                        : reinterpret_cast<const void *>(&crc_stride_kernel<G, 8, 2, kAux, false, true, 3>);
+        if (bf) // byte-table fold (R = 1: the B half of the image is free)
+            return odd ? reinterpret_cast<const void *>(&crc_stride_kernel<G, 8, 2, kAux, true, true>)
+                       : reinterpret_cast<const void *>(&crc_stride_kernel<G, 8, 2, kAux, false, true>);
     }
-    if constexpr (G <= 8) { // byte-table fold (R = 1: the B half of the image is free)
-        if (bf && odd && shape == 0)
-            return reinterpret_cast<const void *>(&crc_stride_kernel<G, 8, 2, kAux, true, true>);
-        if (bf && shape == 0)
-            return reinterpret_cast<const void *>(&crc_stride_kernel<G, 8, 2, kAux, false, true>);
-    }
-    if (odd && shape == 0)
-        return reinterpret_cast<const void *>(&crc_stride_kernel<G, 8, 2, kAux, true>);
-    switch (shape) {
-    case 1: return reinterpret_cast<const void *>(&crc_stride_kernel<G, 4, small ? 2 : 3, kAux>);
-    case 2: return reinterpret_cast<const void *>(&crc_stride_kernel<G, 2, 4, kAux>);
-    case 3: return reinterpret_cast<const void *>(&crc_stride_kernel<G, 4, small ? 3 : 2, kAux>);
-    default: return reinterpret_cast<const void *>(&crc_stride_kernel<G, 8, 2, kAux>);
-    }
+    return odd ? reinterpret_cast<const void *>(&crc_stride_kernel<G, 8, 2, kAux, true>)
+               : reinterpret_cast<const void *>(&crc_stride_kernel<G, 8, 2, kAux>);
 }
 
-const void *stride_fn(int G, int shape, bool odd, bool bf, int prio)
+const void *stride_fn(int G, bool odd, bool bf, int prio)
 {
     switch (G) {
-    case 2: return stride_fn_g<2>(shape, odd, bf, prio);
-    case 4: return stride_fn_g<4>(shape, odd, bf, prio);
-    case 8: return stride_fn_g<8>(shape, odd, bf, prio);
-    case 16: return stride_fn_g<16>(shape, odd, false, prio);
-    case 32: return stride_fn_g<32>(shape, odd, false, prio);
-    default: return stride_fn_g<64>(shape, odd, false, prio);
+    case 2: return stride_fn_g<2>(odd, bf, prio);
+    case 4: return stride_fn_g<4>(odd, bf, prio);
+    case 8: return stride_fn_g<8>(odd, bf, prio);
+    case 16: return stride_fn_g<16>(odd, false, prio);
+    case 32: return stride_fn_g<32>(odd, false, prio);
+    default: return stride_fn_g<64>(odd, false, prio);
     }
 }
 
@@ -951,18 +945,18 @@ const void *stride_fn(int G, int shape, bool odd, bool bf, int prio)
 // rows kernel, so an unbalanced handful of big blocks goes to the fused
 // few-extents kernel, which cuts them into segments (as launch_rows does)
 // G <= 8 (R = 1, set B unused): the sub-KiB byte-fold image, no nibble tables
-bool stride_bf(const priskv_crc_ctx *ctx, int G) { return ctx->small_bf && G <= 8 && ctx->stride_shape == 0; }
+bool stride_bf(const priskv_crc_ctx *ctx, int G) { return ctx->small_bf && G <= 8; }
 
-// progress priority (mode, 0 = off): one 16-wave workgroup per CU, default
-// shape; G <= 8 only with the byte fold, whose tables fit the 64 KiB image
+// progress priority (mode, 0 = off): one 16-wave workgroup per CU; G <= 8
+// only with the byte fold, whose tables fit the 64 KiB image
 int stride_prio_mode(const priskv_crc_ctx *ctx, int G)
 {
-    return (ctx->stride_shape == 0 && (G >= 16 || stride_bf(ctx, G))) ? ctx->stride_prio : 0;
+    return (G >= 16 || stride_bf(ctx, G)) ? ctx->stride_prio : 0;
 }
 
 uint64_t stride_waves(const priskv_crc_ctx *ctx, int G)
 {
-    return stride_prio_mode(ctx, G) ? (uint64_t)ctx->num_cus * 16 : (uint64_t)ctx->num_cus * stride_wgs(ctx, G) * kWaves;
+    return stride_prio_mode(ctx, G) ? (uint64_t)ctx->num_cus * 16 : (uint64_t)ctx->num_cus * stride_wgs(G) * kWaves;
 }
 
 bool stride_segmented(const priskv_crc_ctx *ctx, const StridePlan &P, uint64_t nblocks, uint32_t bs)
@@ -983,7 +977,7 @@ int launch_stride(const priskv_crc_ctx *ctx, const uint8_t *base, uint64_t nbloc
     const bool bf = stride_bf(ctx, P.G);
     const int prio = stride_prio_mode(ctx, P.G);
     const uint64_t nw = prio ? 16 : kWaves;
-    const uint64_t max_wgs = prio ? (uint64_t)ctx->num_cus : (uint64_t)ctx->num_cus * stride_wgs(ctx, P.G);
+    const uint64_t max_wgs = prio ? (uint64_t)ctx->num_cus : (uint64_t)ctx->num_cus * stride_wgs(P.G);
     // a wave's range is one buffer descriptor with 31-bit offsets, and its
     // NB lane groups may run up to NB - 1 blocks past it: cap blocks per launch
     const uint64_t per_wave = ((1ull << 31) - 1) / bs - NB; // >= 1: bs <= kStrideMaxBlock
@@ -991,16 +985,15 @@ int launch_stride(const priskv_crc_ctx *ctx, const uint8_t *base, uint64_t nbloc
     const uint32_t *img = bf ? ctx->d_small_img[log2u((uint32_t)P.G)]
                              : ctx->d_lds_image[P.G == 64 ? 0 : (P.G == 32 ? 1 : 2)]; // set B unused for G < 16
     const uint32_t *nib = ctx->d_nibrep[log2u((uint32_t)P.G)];
-    uint32_t R = P.R, runs = (uint32_t)ctx->stride_runs;
+    uint32_t R = P.R;
     for (uint64_t done = 0; done < nblocks;) {
         uint64_t nb = nblocks - done < cap ? nblocks - done : cap;
         const uint64_t want = (nb + NB * nw - 1) / (NB * nw); // about NB blocks per wave and up
         const uint32_t grid = (uint32_t)(want < max_wgs ? want : max_wgs);
         const uint8_t *b = base + done * bs;
-        const void *fn = stride_fn(P.G, ctx->stride_shape, ctx->stride_funnel && (((uintptr_t)b | bs) & 3u), bf, prio);
+        const void *fn = stride_fn(P.G, (((uintptr_t)b | bs) & 3u) != 0, bf, prio);
         uint32_t *o = out + done;
-        void *args[] = {(void *)&b,   (void *)&nb, (void *)&bs, (void *)&R,
-                        (void *)&img, (void *)&nib, (void *)&o, (void *)&runs};
+        void *args[] = {(void *)&b, (void *)&nb, (void *)&bs, (void *)&R, (void *)&img, (void *)&nib, (void *)&o};
         if (int rc = herr(hipLaunchKernel(fn, dim3(grid), dim3(64 * nw), args, 0, s)))
             return rc;
         done += nb;
@@ -1018,7 +1011,8 @@ int launch_blocks(const priskv_crc_ctx *ctx, const uint8_t *base, uint64_t nbloc
         return launch_head_split(ctx, base, nblocks, bs, out, s);
     if (path == PATH_STRIDE && !stride_to_extents(ctx, base, bs))
         return launch_stride(ctx, base, nblocks, bs, out, s);
-    if (path == PATH_STRIDE) // odd blocks from 4.5 KiB, others from 9 KiB, beyond 64 MiB: extents (segmented when few)
+    if (path == PATH_STRIDE) // odd blocks and others from 9 KiB (odd from 4.5 KiB without progress priority),
+                             // beyond 64 MiB: extents (segmented when few)
         return launch_extents(ctx, base, nblocks, nullptr, nullptr, bs, bs, out, s);
     if (path == PATH_SMALL) {
         const int gl = log2u(bs / 16); // G = 1 << gl
@@ -1026,7 +1020,7 @@ int launch_blocks(const priskv_crc_ctx *ctx, const uint8_t *base, uint64_t nbloc
         const uint64_t nrows = nblocks / per;
         if (nrows) {
             // G >= 2: nibble-table fold (replicated 32-wide tables)
-            const bool bf = ctx->small_bf && gl >= 1 && gl <= 4;
+            const bool bf = small_bf(ctx, gl);
             const uint32_t *fold = gl ? ctx->d_nibrep[gl] : ctx->d_fold;
             const uint32_t *img = bf ? ctx->d_small_img[gl] : ctx->d_lds_image[0];
             const bool prio = ctx->prio;
@@ -1129,12 +1123,12 @@ int priskv_crc32_blocks_path(const void *d_base, uint64_t nblocks, uint32_t bloc
     if (block_size == 0 || (nblocks && !d_base))
         return -EINVAL;
     const int path = choose_path(d_base, block_size);
-    // a default context hashes B = h + whole KiB rows as bodies + heads, and
-    // sends odd blocks from 4.5 KiB, other stride sizes from 9 KiB and blocks
+    // a default context hashes B = h + whole KiB rows as bodies + heads
+    // (unless few large blocks), and sends stride sizes from 9 KiB and blocks
     // beyond 64 MiB to the extents kernel
     if (path == PATH_STRIDE && head_split(nullptr, d_base, nblocks, block_size))
         return PATH_HEAD;
-    if (path == PATH_STRIDE && stride_to_extents_lim(d_base, block_size, kStrideOddMax, kStrideMax, true))
+    if (path == PATH_STRIDE && stride_to_extents_lim(d_base, block_size, kStrideOddMax, kStrideMax))
         return PATH_EXTENTS;
     return path;
 }
@@ -1156,9 +1150,7 @@ int priskv_crc32_blocks_plan(const priskv_crc_ctx *ctx, const void *d_base, uint
         } else if (stride_segmented(ctx, P, nblocks, block_size)) {
             w = snprintf(buf, len, "%s", fused_name);
         } else {
-            const int sh = ctx->stride_shape;
-            const int ch = kStrideShape[sh][0];
-            const int nbuf = sh == 1 ? (P.G < 16 ? 2 : 3) : (sh == 3 ? (P.G < 16 ? 3 : 2) : kStrideShape[sh][1]);
+            const int ch = 8, nbuf = 2;
             const bool bf = stride_bf(ctx, P.G);
             const int pm = stride_prio_mode(ctx, P.G);
             w = snprintf(buf, len,
@@ -1195,13 +1187,52 @@ int priskv_crc32_blocks_plan(const priskv_crc_ctx *ctx, const void *d_base, uint
             w += snprintf(buf + w, len - w, " on the %u-B bodies + crc_head_kernel (%u-B heads)", block_size, hb);
     } else if (path == PATH_SMALL) {
         const uint32_t G = block_size / 16;
-        w = snprintf(buf, len, "crc_small_kernel<G=%u%s>", G, ctx->small_bf && G >= 2 && G <= 16 ? ",byte-fold" : "");
+        w = snprintf(buf, len, "crc_small_kernel<G=%u%s>", G, small_bf(ctx, log2u(G)) ? ",byte-fold" : "");
     } else if (path == PATH_EXTENTS) {
         w = snprintf(buf, len, "%s", extents_desc(ctx, nblocks, block_size));
     } else {
         w = snprintf(buf, len, "crc_generic_kernel");
     }
     return w < 0 ? -EIO : 0;
+}
+
+int priskv_crc_read_roof_dev(const priskv_crc_ctx *ctx, const void *d_base, uint64_t nblocks, uint32_t block_size,
+                             uint32_t *d_sink, void *stream)
+{
+    if (!ctx || block_size == 0 || block_size % 4096 != 0 || ((uintptr_t)d_base & 15) != 0)
+        return -EINVAL;
+    if (nblocks == 0)
+        return 0;
+    if (!d_base || !d_sink)
+        return -EINVAL;
+    DevGuard g(ctx->device);
+    if (!g.ok)
+        return -ENODEV;
+    // the plan the CRC kernel uses for this block size: its pipeline depth,
+    // its resident workgroups and its XCD weights (only with many blocks per
+    // wave, as launch_plan applies them)
+    const int p = plan_for(block_size);
+    const Plan &P = kPlans[p];
+    const uint64_t max_wgs = (uint64_t)ctx->num_cus * ctx->plan_wgs_per_cu[p];
+    const uint64_t cps = block_size / 4096;
+    const uint64_t cap = max_wgs * kWaves * ((1ull << 31) / cps - 1);
+    const uint8_t *base = static_cast<const uint8_t *>(d_base);
+    const void *fn = P.NBUF == 3 ? reinterpret_cast<const void *>(&crc_read_roof_kernel<4, 3, kAux>)
+                                 : reinterpret_cast<const void *>(&crc_read_roof_kernel<4, 2, kAux>);
+    for (uint64_t done = 0; done < nblocks;) {
+        uint64_t n = nblocks - done < cap ? nblocks - done : cap;
+        const uint64_t want = (n + kWaves - 1) / kWaves;
+        const uint32_t grid = (uint32_t)(want < max_wgs ? want : max_wgs);
+        const uint8_t *b = base + done * (uint64_t)block_size;
+        uint32_t *o = d_sink + done;
+        uint32_t bs = block_size;
+        uint32_t xw = n >= 32ull * grid * kWaves ? ctx->plan_xw[p] : 0u;
+        void *args[] = {(void *)&b, (void *)&n, (void *)&bs, (void *)&o, (void *)&xw};
+        if (int rc = herr(hipLaunchKernel(fn, dim3(grid), dim3(kThreads), args, 0, (hipStream_t)stream)))
+            return rc;
+        done += n;
+    }
+    return 0;
 }
 
 int priskv_crc_ctx_create(int device, priskv_crc_ctx **out)
@@ -1245,10 +1276,6 @@ int priskv_crc_ctx_create(int device, priskv_crc_ctx **out)
         c->head_split = !(hs && !strcmp(hs, "0"));
         const char *sb = getenv("PRISKV_CRC_SMALL_BF");
         c->small_bf = !(sb && !strcmp(sb, "0"));
-        const char *fc = getenv("PRISKV_CRC_FUSED_CH");
-        c->fused_ch = fc ? atoi(fc) : kFusedCh;
-        if (c->fused_ch != 2 && c->fused_ch != 4 && c->fused_ch != 8)
-            c->fused_ch = kFusedCh;
         const char *fe = getenv("PRISKV_CRC_FUSED");
         c->fused = !(fe && !strcmp(fe, "0"));
         const char *se = getenv("PRISKV_CRC_STRIDE");
@@ -1258,23 +1285,11 @@ int priskv_crc_ctx_create(int device, priskv_crc_ctx **out)
             const int v = atoi(m);
             c->stride_g = (v >= 2 && v <= 64 && !(v & (v - 1))) ? v : 0;
         }
-        c->stride_shape = 0;
-        if (const char *m = getenv("PRISKV_CRC_STRIDE_SHAPE"))
-            c->stride_shape = atoi(m) & 3;
-        const char *fu = getenv("PRISKV_CRC_STRIDE_FUNNEL");
-        c->stride_funnel = !(fu && !strcmp(fu, "0"));
-        const char *re = getenv("PRISKV_CRC_STRIDE_RUNS");
-        c->stride_runs = re && !strcmp(re, "1");
+        c->stride_prio = c->prio ? 3 : 0; // PRISKV_CRC_PRIO=0 turns it off with the others
         c->stride_max = kStrideMax;
-        c->stride_odd_max = kStrideOddMax;
+        c->stride_odd_max = c->stride_prio ? kStrideOddMax : kStrideOddMaxNoPrio;
         if (const char *m = getenv("PRISKV_CRC_STRIDE_MAX_KIB"))
             c->stride_max = c->stride_odd_max = strtoull(m, nullptr, 10) << 10;
-        c->stride_wgs = 2;
-        c->stride_prio = c->prio ? 3 : 0; // PRISKV_CRC_PRIO=0 turns it off with the others
-        if (const char *m = getenv("PRISKV_CRC_STRIDE_PRIO"))
-            c->stride_prio = atoi(m) ? 3 : 0;
-        if (const char *m = getenv("PRISKV_CRC_STRIDE_WGS"))
-            c->stride_wgs = atoi(m) == 1 ? 1 : 2;
         c->seg_max_extents = kSegMaxExtents;
         c->tile_min_bytes = kTileMinBytes;
         c->tile_bytes = kTileBytes;

@@ -618,6 +618,32 @@ def test_head_split_blocks(torch_cuda, ctx, bs):
     off_ctx.close()
 
 
+@pytest.mark.parametrize("bs", [(1023 << 10) + 4, (127 << 10) + 64, (96 << 10) + 12])
+def test_head_split_few_large_odd_kib_bodies(torch_cuda, ctx, bs):
+    """A few head + body blocks whose body is an odd number of KiB >= 64 KiB:
+    the rows kernel cannot cut such bodies into whole-KiB segments, so the
+    batch must not take the head split (one wave per block would stream at a
+    few GB/s) but the extents path, which the fused kernel segments.  Plan
+    and every CRC against the oracle (sentinel-filled output), for 1 to 9
+    blocks; a balanced batch of the same size does take the head split."""
+    torch = torch_cuda
+    sentinel = int(np.int32(np.uint32(0xA5A5A5A5).view(np.int32)))
+    for nb in (1, 2, 9):
+        t = _region(torch, ctx, bs * nb + 16, SEED ^ (bs + nb), nb)
+        view = t[4:4 + bs * nb]
+        plan = ctx.blocks_plan(view.data_ptr(), nb, bs)
+        assert "crc_head_kernel" not in plan and plan.startswith("crc_ranges_fused_kernel"), plan
+        out = torch.full((nb,), sentinel, dtype=torch.int32, device="cuda")
+        ctx.blocks_dev(view, bs, out=out)
+        torch.cuda.synchronize()
+        want = O.crc32_blocks(view.cpu().numpy(), bs, nthreads=8)
+        got = _u32(out)
+        assert np.array_equal(got, want), (bs, nb, np.nonzero(got != want)[0][:8])
+        del t
+    nbal = 2 * torch.cuda.get_device_properties(0).multi_processor_count * 8  # two blocks per rows-kernel wave
+    assert "crc_head_kernel" in ctx.blocks_plan(4096, nbal, bs)
+
+
 def test_ranges_many_shape_chunk_sizes(torch_cuda, ctx):
     """The 16-wave many-extents shape sizes each wave's chunks from its own
     extents (8, 4 or 2 rows: crc_device.inc OPT bit 14).  Three populations
@@ -1282,15 +1308,6 @@ def ctx_fused16k(torch_cuda):
     c.close()
 
 
-@pytest.fixture(scope="module")
-def ctx_fused_wide(torch_cuda):
-    """The fused kernel with 4- and 8-row chunks (PRISKV_CRC_FUSED_CH)."""
-    cs = [_ctx_env(PRISKV_CRC_SEG_MAX_EXTENTS=16384, PRISKV_CRC_FUSED_CH=ch) for ch in (4, 8)]
-    yield cs
-    for c in cs:
-        c.close()
-
-
 _FUSED_CASES = [
     [256 << 20],                                  # a lone huge value: every workgroup holds part of it
     [(1 << 14) + 1],                              # two segments, the last one byte
@@ -1308,7 +1325,7 @@ _FUSED_CASES = [
 
 
 @pytest.mark.parametrize("case", range(len(_FUSED_CASES) + 2))
-def test_fused_few_extents(torch_cuda, ctx_fused16k, ctx_threelaunch, ctx_fused_wide, case):
+def test_fused_few_extents(torch_cuda, ctx_fused16k, ctx_threelaunch, case):
     """The one-launch few-extents kernel (plan in LDS, per-extent counters,
     last-arriver combine) equals the oracle and the three-launch path, at
     ragged offsets on a 16-B-misaligned base, called repeatedly (the counters
@@ -1335,7 +1352,7 @@ def test_fused_few_extents(torch_cuda, ctx_fused16k, ctx_threelaunch, ctx_fused_
     d_o = torch.from_numpy(o.astype(np.int64)).cuda()
     d_l = torch.from_numpy(lens.view(np.int32)).cuda()
     want = O.crc32_ranges(base[:n].cpu().numpy(), o, lens)
-    for c in [ctx_fused16k, ctx_threelaunch] + ctx_fused_wide:
+    for c in (ctx_fused16k, ctx_threelaunch):
         for _ in range(3):
             got = _u32(c.ranges_dev(base, d_o, d_l))
             torch.cuda.synchronize()
@@ -1401,20 +1418,21 @@ _STRIDE_SIZES = {2: [16, 17, 23, 32], 4: [33, 48, 50, 64], 8: [65, 100, 127, 128
 
 
 @pytest.mark.parametrize("G", sorted(_STRIDE_SIZES))
-def test_stride_kernel_every_g_and_shape(torch_cuda, G):
+def test_stride_kernel_every_g_and_variant(torch_cuda, G):
     """crc_stride_kernel (odd block sizes, unaligned bases) for every lane
-    count G (forced, PRISKV_CRC_STRIDE_G) and chunk shape
-    (PRISKV_CRC_STRIDE_SHAPE 0-3): the oracle's CRCs at base misalignments 0,
-    3 and 4, for batches of 1 block, a ragged last group, and several groups
-    per wave with a ragged end."""
+    count G (forced, PRISKV_CRC_STRIDE_G) and every variant the library
+    ships: progress priority in one 16-wave workgroup or two 8-wave
+    workgroups (PRISKV_CRC_PRIO=0), byte or nibble fold (G <= 8,
+    PRISKV_CRC_SMALL_BF=0), aligned or funnel-shift loads: the oracle's CRCs
+    at base misalignments 0, 3 and 4, for batches of 1 block, a ragged last
+    group, and several groups per wave with a ragged end."""
     torch = torch_cuda
     hs = {"PRISKV_CRC_HEADSPLIT": 0}  # 4100 B and the like stay on the stride kernel
-    ctxs = [_ctx_env(PRISKV_CRC_STRIDE_G=G, PRISKV_CRC_STRIDE_SHAPE=sh, **hs) for sh in range(4)]
-    ctxs.append(_ctx_env(PRISKV_CRC_STRIDE_G=G, PRISKV_CRC_STRIDE_RUNS=1, **hs))  # G >= 16: groups in runs
-    ctxs.append(_ctx_env(PRISKV_CRC_STRIDE_G=G, PRISKV_CRC_STRIDE_FUNNEL=0, **hs))  # odd sizes: unaligned loads
-    ctxs.append(_ctx_env(PRISKV_CRC_STRIDE_G=G, PRISKV_CRC_STRIDE_MAX_KIB=131072, **hs))  # large blocks stay here
-    ctxs.insert(1, _ctx_env(PRISKV_CRC_STRIDE_G=G, PRISKV_CRC_SMALL_BF=0, **hs))  # G <= 8: nibble fold
-    ctxs.insert(2, _ctx_env(PRISKV_CRC_STRIDE_G=G, PRISKV_CRC_STRIDE_PRIO=0, **hs))  # two 8-wave workgroups
+    ctxs = [_ctx_env(PRISKV_CRC_STRIDE_G=G, **hs),
+            _ctx_env(PRISKV_CRC_STRIDE_G=G, PRISKV_CRC_SMALL_BF=0, **hs),  # G <= 8: nibble fold
+            _ctx_env(PRISKV_CRC_STRIDE_G=G, PRISKV_CRC_PRIO=0, **hs),  # two 8-wave workgroups
+            _ctx_env(PRISKV_CRC_STRIDE_G=G, PRISKV_CRC_PRIO=0, PRISKV_CRC_SMALL_BF=0, **hs),
+            _ctx_env(PRISKV_CRC_STRIDE_G=G, PRISKV_CRC_STRIDE_MAX_KIB=131072, **hs)]  # large blocks stay here
     per = 64 // G
     rng = np.random.default_rng(G)
     try:

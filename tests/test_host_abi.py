@@ -234,7 +234,14 @@ def test_path_selection():
     assert C.blocks_path(4098, 10, 4100) == "stride"      # 2-byte aligned base
     assert C.blocks_path(4096, 10, 1024 + 64) == "headsplit"
     assert C.blocks_path(4096, 10, 1024 + 68) == "stride"  # head above 64 B
-    assert C.blocks_path(4096, 10, (64 << 10) + 4) == "headsplit"
+    # few large head + body blocks: the rows kernel does not segment the
+    # bodies, so they keep the extents path (segmented by the fused kernel)
+    assert C.blocks_path(4096, 10, (64 << 10) + 4) == "extents"
+    assert C.blocks_path(4096, 10, (1023 << 10) + 4) == "extents"
+    assert C.blocks_path(4096, 3000, (64 << 10) + 4) == "extents"     # 3000 over 2048 waves: unbalanced
+    assert C.blocks_path(4096, 4096, (64 << 10) + 4) == "headsplit"   # 2 per wave: balanced
+    assert C.blocks_path(4096, 1 << 16, (64 << 10) + 4) == "headsplit"
+    assert C.blocks_path(4096, 10, (32 << 10) + 4) == "headsplit"      # bodies below 64 KiB
     assert C.blocks_path(4096, 10, 4097) == "stride"      # odd
     assert C.blocks_path(4096, 10, 1000) == "stride"
     assert C.blocks_path(4097, 10, 256) == "stride"     # sub-KiB power of two, unaligned base

@@ -18,6 +18,7 @@
 #   libenv:VAR=V:ARGS     the same with one environment variable set
 #   py:SCRIPT[:ARGS]      python tools/SCRIPT ARGS (commas for spaces)
 #   gloo2[:A,B,...]       2-rank rehearsal of bench.py's N>1 path on this one GPU (gloo)
+#   gloo:N[:A,B,...]      the same with N ranks
 #   ktrace[:A,B,...]      rocprofv3 --kernel-trace --stats over bench.py A B ...
 #   ktracepy:SCRIPT[:A,B] rocprofv3 --kernel-trace --stats over python tools/SCRIPT A B ...
 #   pmc:C1+C2[:A,B,...]   one rocprofv3 --pmc pass (counters C1 C2 ...) over bench.py A B ...
@@ -89,6 +90,15 @@ for step in "$@"; do
         PRISKV_BENCH_REHEARSAL=1 timeout -k 10 400 python -m torch.distributed.run --nnodes 1 --nproc-per-node 2 \
             --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 2 ${arg//,/ } > "$O/gloo2_$n.json" \
             2> "$O/gloo2_$n.err"
+        ;;
+    gloo)
+        # gloo:N[:A,B,...] -- N-rank rehearsal of bench.py's N>1 path on this one GPU (gloo)
+        nr=${arg%%:*}
+        bargs=""
+        [[ "$arg" == *:* ]] && bargs=${arg#*:}
+        PRISKV_BENCH_REHEARSAL=1 timeout -k 10 900 python -m torch.distributed.run --nnodes 1 --nproc-per-node "$nr" \
+            --master-addr 127.0.0.1 --master-port 29521 bench.py --gpus "$nr" ${bargs//,/ } > "$O/gloo${nr}_$n.json" \
+            2> "$O/gloo${nr}_$n.err"
         ;;
     oversub)
         set +e
