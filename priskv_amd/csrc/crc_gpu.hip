@@ -69,6 +69,7 @@ struct priskv_crc_ctx {
     int plan_wgs_per_cu[8];    // resident workgroups per CU of each rows-kernel plan
     uint32_t plan_xw[8];       // rows-kernel split per plan: (even << 16) | odd XCD weight, 0 = equal
     int segment;               // split few large blocks / extents into segments (PRISKV_CRC_SEGMENT=0: off)
+    int split;                 // rows kernel split mode for few blocks per wave (PRISKV_CRC_SPLIT=0: off)
     int prio;                  // rows kernel progress priority (PRISKV_CRC_PRIO=0: off)
     int balance;               // byte-balanced extents split (PRISKV_CRC_BALANCE=0: off)
     int ext_adapt;             // per-wave chunk size of the many-extents shape (PRISKV_CRC_EXT_ADAPT=0: 2 rows)
@@ -444,31 +445,44 @@ int plan_for(uint32_t bs)
     return R % 2 == 0 ? PLAN_G64_CH2 : PLAN_G64_CH1;
 }
 
+constexpr int prio_free(int opt) { return opt & ~(3 << 8); }
+
 template <int G, int CH, int NB, int OPT>
 const void *plan_kernel()
 {
     return reinterpret_cast<const void *>(&crc_rows_kernel<G, CH, NB, kAux, OPT>);
 }
 
-// prio = false: the plan's kernel without progress priority (PRISKV_CRC_PRIO=0)
+// prio = false: the plan's kernel without progress priority (PRISKV_CRC_PRIO=0);
+// split: its split-mode instance (plans with one block per wave group and an
+// unpipelined fold: plan_splits)
+constexpr int kSplitOpt = 64;
+constexpr bool plan_splits(int p) { return kPlans[p].G == 64 && !(kPlans[p].opt & 2); }
+
 template <int P>
-const void *plan_kernel_p(bool prio)
+const void *plan_kernel_p(bool prio, bool split)
 {
     constexpr Plan Q = kPlans[P];
-    return prio ? plan_kernel<Q.G, Q.CH, Q.NBUF, Q.opt>() : plan_kernel<Q.G, Q.CH, Q.NBUF, (Q.opt & ~(3 << 8))>();
+    constexpr int O = prio_free(Q.opt);
+    if constexpr (plan_splits(P)) {
+        if (split)
+            return prio ? plan_kernel<Q.G, Q.CH, Q.NBUF, Q.opt | kSplitOpt>()
+                        : plan_kernel<Q.G, Q.CH, Q.NBUF, O | kSplitOpt>();
+    }
+    return prio ? plan_kernel<Q.G, Q.CH, Q.NBUF, Q.opt>() : plan_kernel<Q.G, Q.CH, Q.NBUF, O>();
 }
 
-const void *plan_fn(int p, bool prio)
+const void *plan_fn(int p, bool prio, bool split = false)
 {
     switch (p) {
-    case PLAN_4K: return plan_kernel_p<PLAN_4K>(prio);
-    case PLAN_G64_CH4_NIB: return plan_kernel_p<PLAN_G64_CH4_NIB>(prio);
-    case PLAN_G16_CH4_PIPE: return plan_kernel_p<PLAN_G16_CH4_PIPE>(prio);
-    case PLAN_G16_CH4: return plan_kernel_p<PLAN_G16_CH4>(prio);
-    case PLAN_G64_CH4: return plan_kernel_p<PLAN_G64_CH4>(prio);
-    case PLAN_G64_CH4_BIG: return plan_kernel_p<PLAN_G64_CH4_BIG>(prio);
-    case PLAN_G64_CH2: return plan_kernel_p<PLAN_G64_CH2>(prio);
-    default: return plan_kernel_p<PLAN_G64_CH1>(prio);
+    case PLAN_4K: return plan_kernel_p<PLAN_4K>(prio, split);
+    case PLAN_G64_CH4_NIB: return plan_kernel_p<PLAN_G64_CH4_NIB>(prio, split);
+    case PLAN_G16_CH4_PIPE: return plan_kernel_p<PLAN_G16_CH4_PIPE>(prio, split);
+    case PLAN_G16_CH4: return plan_kernel_p<PLAN_G16_CH4>(prio, split);
+    case PLAN_G64_CH4: return plan_kernel_p<PLAN_G64_CH4>(prio, split);
+    case PLAN_G64_CH4_BIG: return plan_kernel_p<PLAN_G64_CH4_BIG>(prio, split);
+    case PLAN_G64_CH2: return plan_kernel_p<PLAN_G64_CH2>(prio, split);
+    default: return plan_kernel_p<PLAN_G64_CH1>(prio, split);
     }
 }
 
@@ -492,9 +506,12 @@ uint32_t tile_groups(const priskv_crc_ctx *ctx, uint64_t ngroups, uint64_t gstri
     return t ? (uint32_t)(t < (1u << 20) ? t : (1u << 20)) : 1u;
 }
 
-// stride: bytes from block to block (0: bs; more for the head-split bodies)
+// stride: bytes from block to block (0: bs; more for the head-split bodies).
+// split > 1: the split mode (ngroups = blocks; cnt / xacc: zeroed scratch of
+// ngroups words each, left zero), one launch
 int launch_plan(const priskv_crc_ctx *ctx, int p, const uint8_t *base, uint64_t ngroups, uint32_t bs, uint32_t *out,
-                hipStream_t s, uint32_t stride = 0)
+                hipStream_t s, uint32_t stride = 0, uint32_t split = 1, uint32_t *cnt = nullptr,
+                uint32_t *xacc = nullptr)
 {
     if (!stride)
         stride = bs;
@@ -503,6 +520,19 @@ int launch_plan(const priskv_crc_ctx *ctx, int p, const uint8_t *base, uint64_t 
     const uint64_t max_wgs = (uint64_t)ctx->num_cus * ctx->plan_wgs_per_cu[p];
     const uint64_t nb_per_group = 64 / P.G;
     const uint64_t cps = bs / ((uint64_t)P.CH * 16u * P.G);
+    const uint32_t *img = ctx->d_lds_image[gi];
+    const uint32_t *fold = (P.opt & 32) ? ctx->d_nibrep[log2u(P.G)] : ctx->d_fold + log2u(P.G) * 2048;
+    const uint32_t *zp = ctx->d_zpow;
+    if (split > 1) { // one launch over ngroups * split units (host-checked: < 2^31 chunks per wave)
+        uint64_t n = ngroups * split;
+        const uint64_t want = (n + kWaves - 1) / kWaves;
+        const uint32_t grid = (uint32_t)(want < max_wgs ? want : max_wgs);
+        uint32_t xw = n >= 32ull * grid * kWaves ? ctx->plan_xw[p] : 0u, tile = 0;
+        void *args[] = {(void *)&base, (void *)&n,    (void *)&bs,    (void *)&img,   (void *)&fold,
+                        (void *)&out,  (void *)&xw,   (void *)&tile,  (void *)&stride, (void *)&split,
+                        (void *)&zp,   (void *)&cnt,  (void *)&xacc};
+        return herr(hipLaunchKernel(plan_fn(p, ctx->prio, true), dim3(grid), dim3(kThreads), args, 0, s));
+    }
     // the kernel counts a wave's chunks in 32 bits: cap groups per launch
     const uint64_t cap = max_wgs * kWaves * ((1ull << 31) / cps - 1);
     for (uint64_t done = 0; done < ngroups;) {
@@ -511,13 +541,14 @@ int launch_plan(const priskv_crc_ctx *ctx, int p, const uint8_t *base, uint64_t 
         const uint32_t grid = (uint32_t)(want < max_wgs ? want : max_wgs);
         const uint8_t *b = base + done * nb_per_group * stride;
         uint32_t *o = out + done * nb_per_group;
-        const uint32_t *img = ctx->d_lds_image[gi];
-        const uint32_t *fold = (P.opt & 32) ? ctx->d_nibrep[log2u(P.G)] : ctx->d_fold + log2u(P.G) * 2048;
         // weights move whole groups: only worth it with many groups per wave
         uint32_t xw = n >= 32ull * grid * kWaves ? ctx->plan_xw[p] : 0u;
         uint32_t tile = tile_groups(ctx, n, nb_per_group * stride);
-        void *args[] = {(void *)&b, (void *)&n,  (void *)&bs,   (void *)&img,   (void *)&fold,
-                        (void *)&o, (void *)&xw, (void *)&tile, (void *)&stride};
+        uint32_t one = 1;
+        uint32_t *none = nullptr;
+        void *args[] = {(void *)&b,  (void *)&n,    (void *)&bs,   (void *)&img,    (void *)&fold,
+                        (void *)&o,  (void *)&xw,   (void *)&tile, (void *)&stride, (void *)&one,
+                        (void *)&zp, (void *)&none, (void *)&none};
         if (int rc = herr(hipLaunchKernel(plan_fn(p, ctx->prio), dim3(grid), dim3(kThreads), args, 0, s)))
             return rc;
         done += n;
@@ -554,6 +585,42 @@ uint32_t segments_for(const priskv_crc_ctx *ctx, uint64_t nblocks, uint32_t bs)
 
 int launch_rows_plain(const priskv_crc_ctx *ctx, const uint8_t *base, uint64_t nblocks, uint32_t bs, uint32_t *out,
                       hipStream_t s, uint32_t stride = 0);
+
+// Split mode (crc_rows_kernel OPT bit 6): a balanced batch with
+// fewer than kSplitUnitsPerWave blocks per wave (1 MiB blocks: 2) cannot take
+// the XCD weights, which move whole blocks.  Cut each block into S units
+// (S a power of two, units of whole 4 KiB chunks and >= kSplitMinUnit) until
+// there are kSplitUnitsPerWave units per wave, and the weights apply to
+// units; parts of blocks combine inside the launch.  1 = no split (the
+// weights already apply or are off, no such S, PRISKV_CRC_SPLIT=0).
+constexpr uint64_t kSplitUnitsPerWave = 32;
+constexpr uint32_t kSplitMinUnit = 16u << 10;
+
+uint32_t split_for(const priskv_crc_ctx *ctx, uint64_t nblocks, uint32_t bs)
+{
+    const int p = plan_for(bs);
+    if (!ctx->split || !plan_splits(p) || !ctx->plan_xw[p] || bs % 4096 != 0)
+        return 1;
+    const uint64_t want = kSplitUnitsPerWave * (uint64_t)ctx->num_cus * ctx->plan_wgs_per_cu[p] * kWaves;
+    if (nblocks >= want)
+        return 1;
+    uint32_t S = 1;
+    while (nblocks * S < want && (bs / 4096) % (2 * S) == 0 && bs / (2 * S) >= kSplitMinUnit)
+        S *= 2;
+    return nblocks * S >= want ? S : 1;
+}
+
+int launch_split(const priskv_crc_ctx *ctx, const uint8_t *base, uint64_t nblocks, uint32_t bs, uint32_t S,
+                 uint32_t *out, hipStream_t s)
+{
+    Scratch sc(ctx, s, ctx->cnt_pool, true); // zero at rest: the kernel leaves it zero
+    if (int rc = sc.get((size_t)nblocks * 8))
+        return rc;
+    uint32_t *cnt = static_cast<uint32_t *>(sc.p);
+    const int rc = launch_plan(ctx, plan_for(bs), base, nblocks, bs, out, s, 0, S, cnt, cnt + nblocks);
+    const int frc = sc.release();
+    return rc ? rc : frc;
+}
 
 // Few extents: the same kernel over segments of each extent.  The segments
 // are laid out on the device by crc_seg_plan_kernel (the host never sees
@@ -685,8 +752,11 @@ int launch_rows(const priskv_crc_ctx *ctx, const uint8_t *base, uint64_t nblocks
                 hipStream_t s)
 {
     const uint32_t S = segments_for(ctx, nblocks, bs);
-    if (S == 1)
-        return launch_rows_plain(ctx, base, nblocks, bs, out, s);
+    if (S == 1) {
+        const uint32_t sp = split_for(ctx, nblocks, bs);
+        return sp > 1 ? launch_split(ctx, base, nblocks, bs, sp, out, s)
+                      : launch_rows_plain(ctx, base, nblocks, bs, out, s);
+    }
     // few large blocks: the fused few-extents kernel in one launch (1 x 256 MiB
     // 50 us against 55-57 for rows + combine, 1024 x 1 MiB level: DESIGN §4)
     if (fused_blocks(ctx, nblocks))
@@ -1175,7 +1245,11 @@ int priskv_crc32_blocks_plan(const priskv_crc_ctx *ctx, const void *d_base, uint
             w += snprintf(buf + w, len - w, ",progress-priority %d", mode);
         const uint64_t ngroups = nblocks * S / (64 / P.G);
         const uint32_t tile = tile_groups(ctx, ngroups, (uint64_t)(64 / P.G) * bs);
-        if (w >= 0 && (uint64_t)w < len && tile)
+        const uint32_t sp = (S == 1 && !hb) ? split_for(ctx, nblocks, bs) : 1u;
+        if (w >= 0 && (uint64_t)w < len && sp > 1)
+            w += snprintf(buf + w, len - w, ",split %u units of %u B per block,xcd-weighted %u:%u", sp, bs / sp,
+                          xw >> 16, xw & 0xFFFF);
+        else if (w >= 0 && (uint64_t)w < len && tile)
             w += snprintf(buf + w, len - w, ",block-cyclic tiles of %u groups", tile);
         else if (w >= 0 && (uint64_t)w < len && xw && ngroups >= 32ull * ctx->num_cus * ctx->plan_wgs_per_cu[p] * kWaves)
             w += snprintf(buf + w, len - w, ",xcd-weighted %u:%u", xw >> 16, xw & 0xFFFF);
@@ -1266,6 +1340,8 @@ int priskv_crc_ctx_create(int device, priskv_crc_ctx **out)
     {
         const char *e = getenv("PRISKV_CRC_SEGMENT");
         c->segment = !(e && !strcmp(e, "0"));
+        const char *sp = getenv("PRISKV_CRC_SPLIT");
+        c->split = !(sp && !strcmp(sp, "0"));
         const char *pe = getenv("PRISKV_CRC_PRIO");
         c->prio = !(pe && !strcmp(pe, "0"));
         const char *be = getenv("PRISKV_CRC_BALANCE");

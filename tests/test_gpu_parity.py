@@ -988,6 +988,40 @@ def test_full_config_1M_x_4K(torch_cuda, ctx):
     assert np.array_equal(_u32(out), want)
 
 
+# (block size, blocks): balanced batches with few blocks per wave; 1900 x
+# 1 MiB gives fewer units per wave than units per block (waves whose whole
+# range lies inside one block)
+_SPLIT_CASES = [(1 << 20, 1900), (1 << 20, 4096), (512 << 10, 4000), (256 << 10, 6000), (1 << 20, 2048)]
+
+
+@pytest.mark.parametrize("bs,nb", _SPLIT_CASES)
+def test_rows_split_mode(torch_cuda, ctx, bs, nb):
+    """crc_rows_kernel's split mode (OPT bit 6): few blocks per wave cut into
+    units so the XCD weights apply; parts of blocks combine through two
+    zero-at-rest words per block inside the launch.  Every CRC against the
+    oracle, sentinel-filled output, three launches back to back (the scratch
+    must be left zero), and against a context with the split off."""
+    torch = torch_cuda
+    t = _region(torch, ctx, bs * nb, SEED ^ (bs + nb), 3)
+    view = t[:bs * nb]
+    plan = ctx.blocks_plan(view.data_ptr(), nb, bs)
+    xcd = "xcd-weighted" in ctx.blocks_plan(view.data_ptr(), 1 << 20, 4096)  # the probe saw round-robin XCDs
+    assert ("split" in plan) == xcd, plan
+    want = O.crc32_blocks(view.cpu().numpy(), bs, nthreads=16)
+    off = _ctx_env(PRISKV_CRC_SPLIT=0)
+    try:
+        assert "split" not in off.blocks_plan(view.data_ptr(), nb, bs)
+        sentinel = int(np.int32(np.uint32(0xA5A5A5A5).view(np.int32)))
+        for c in (ctx, ctx, ctx, off):
+            out = torch.full((nb,), sentinel, dtype=torch.int32, device="cuda")
+            c.blocks_dev(view, bs, out=out)
+            torch.cuda.synchronize()
+            got = _u32(out)
+            assert np.array_equal(got, want), (bs, nb, plan, np.nonzero(got != want)[0][:8])
+    finally:
+        off.close()
+
+
 @pytest.mark.slow
 @pytest.mark.parametrize("bs", [65536, 1 << 20])
 def test_full_sweep_4GiB(torch_cuda, ctx, bs):

@@ -24,6 +24,7 @@
 #   pmc:C1+C2[:A,B,...]   one rocprofv3 --pmc pass (counters C1 C2 ...) over bench.py A B ...
 #   pmcpy:C1+C2:SCRIPT[:A,B]  one --pmc pass over python tools/SCRIPT A B ...
 #   pmclib:C1+C2:ARGS     one --pmc pass over tools/lib_timing ARGS (no torch in the process)
+#   probe:ENV2:ARGS       tools/alloc_probe ARGS, second context with ENV2 (A/B, same allocations)
 #   pmcprobe:C1+C2:ARGS   one --pmc pass over tools/alloc_probe ARGS
 #   ktracelib:ARGS        rocprofv3 --kernel-trace --stats over tools/lib_timing ARGS
 #   oversub               bench.py as 2 ranks on this one GPU WITHOUT the rehearsal
@@ -145,6 +146,15 @@ for step in "$@"; do
         (cd /tmp && export TMPDIR=/tmp &&
             timeout -s KILL 120 rocprofv3 --pmc ${ctrs//+/ } -d "$O/pmclib_$n" -o run --output-format csv \
                 -- "$R/tools/lib_timing" ${largs//,/ } > "$O/pmclib_$n.out" 2> "$O/pmclib_$n.err")
+        ;;
+    probe)
+        # probe:VAR=V[;VAR=V]:ARGS -- tools/alloc_probe ARGS with a second context (ALLOC_PROBE_ENV2): an A/B
+        # on the same allocations in one process
+        e2=${arg%%:*}
+        largs=""
+        [[ "$arg" == *:* ]] && largs=${arg#*:}
+        ALLOC_PROBE_ENV2="$e2" timeout -k 10 300 ./tools/alloc_probe ${largs//,/ } > "$O/probe_$n.jsonl" \
+            2> "$O/probe_$n.err"
         ;;
     pmcprobe)
         ctrs=${arg%%:*}
