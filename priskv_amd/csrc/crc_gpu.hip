@@ -109,6 +109,8 @@ struct priskv_crc_ctx {
     // allocated; the kernel leaves the counters zero; guarded by pool_lock)
     mutable priskv_crc_pool_slot cnt_pool[NPOOL];
     int fused;                 // few extents in one launch (PRISKV_CRC_FUSED=0: the three-launch path)
+    int fused_xw;              // fused kernel: XCD-weighted split of finer segments (PRISKV_CRC_FUSED_XW=0: off)
+    int fused_early;           // fused kernel: first chunks before the tables (PRISKV_CRC_FUSED_EARLY=0: off)
     int stride;                // odd block sizes / unaligned bases take crc_stride_kernel (PRISKV_CRC_STRIDE=0: the
                                // extents / generic kernels, as in round 2)
     int stride_g;              // PRISKV_CRC_STRIDE_G: force the stride kernel's G (0 = cost model; tests)
@@ -651,6 +653,8 @@ constexpr uint32_t kSegMinLen = 64u << 10;
 // progress priority off in the fused kernel: 1 x 256 MiB 49.7 us vs 50.7 with
 // mode 3, 4096 small values 7.6 vs 7.7 us (profiles/r02/fused/ktrace_shapes_*)
 constexpr int kFusedPrio = 0;
+constexpr uint64_t kFusedUnitsPerWave = 32; // with XCD weights (fused_xw)
+constexpr uint32_t kFusedMinShift = 10;     // ... segments of at least 1 KiB
 
 // one segment size per call (crc_seg_plan_kernel / the fused kernel): about
 // kSegPerWave full segments per resident wave, so the count split of
@@ -690,15 +694,25 @@ int launch_fused(const priskv_crc_ctx *ctx, const uint8_t *base, uint64_t n, con
     const uint64_t sh = (uintptr_t)base & 15;
     const uint8_t *abase = base - sh;
     const uint32_t *lens_or_null = offs ? lens : nullptr;
-    const uint32_t tgt = 1u << (31 - __builtin_clz((uint32_t)seg_target(ctx))); // the kernel takes a power of two
+    // XCD weights (fused_xw): segments of >= 1 KiB, about kFusedUnitsPerWave per
+    // resident wave, so that the weights (whole units) apply to large calls;
+    // else about kSegPerWave of >= 16 KiB (round 3)
+    const uint64_t waves = (uint64_t)ctx->num_cus * kFusedWaves;
+    const uint64_t want = ctx->fused_xw ? kFusedUnitsPerWave * waves : seg_target(ctx);
+    const uint32_t tgt = 1u << (31 - __builtin_clz((uint32_t)std::min<uint64_t>(want, 1u << 30))); // a power of two
+    uint32_t ms = ctx->fused_xw ? kFusedMinShift : kSegMinShift;
+    uint32_t xw = ctx->fused_xw ? ctx->plan_xw[PLAN_4K] : 0u;
     // 2-row chunks: 4 and 8 rows lost 6-13 % on a lone 256 MiB value (profiles/r03/fused/)
     const void *fn =
-        reinterpret_cast<const void *>(&crc_ranges_fused_kernel<kExtRows, kNbuf, kAux, kFusedPrio, kFusedWaves>);
+        ctx->fused_early
+            ? reinterpret_cast<const void *>(
+                  &crc_ranges_fused_kernel<kExtRows, kNbuf, kAux, kFusedPrio, kFusedWaves, true>)
+            : reinterpret_cast<const void *>(&crc_ranges_fused_kernel<kExtRows, kNbuf, kAux, kFusedPrio, kFusedWaves>);
     const uint32_t *img = ctx->d_lds_image[0], *nib = ctx->d_nib16, *rs = ctx->d_rowshift, *zp = ctx->d_zpow;
-    uint32_t ms = kSegMinShift;
     void *args[] = {(void *)&abase, (void *)&n,   (void *)&offs, (void *)&lens_or_null, (void *)&sh,
                     (void *)&stride, (void *)&len_const, (void *)&img, (void *)&nib, (void *)&rs,
-                    (void *)&out,   (void *)&zp,  (void *)&tgt, (void *)&ms, (void *)&cnt, (void *)&xacc};
+                    (void *)&out,   (void *)&zp,  (void *)&tgt, (void *)&ms, (void *)&cnt, (void *)&xacc,
+                    (void *)&xw};
     const int rc = herr(hipLaunchKernel(fn, dim3(grid), dim3(64 * kFusedWaves), args, 0, s));
     const int frc = sc.release();
     return rc ? rc : frc;
@@ -1354,6 +1368,10 @@ int priskv_crc_ctx_create(int device, priskv_crc_ctx **out)
         c->small_bf = !(sb && !strcmp(sb, "0"));
         const char *fe = getenv("PRISKV_CRC_FUSED");
         c->fused = !(fe && !strcmp(fe, "0"));
+        const char *fx = getenv("PRISKV_CRC_FUSED_XW");
+        c->fused_xw = !(fx && !strcmp(fx, "0"));
+        const char *fy = getenv("PRISKV_CRC_FUSED_EARLY");
+        c->fused_early = !(fy && !strcmp(fy, "0"));
         const char *se = getenv("PRISKV_CRC_STRIDE");
         c->stride = !(se && !strcmp(se, "0"));
         c->stride_g = 0;

@@ -1342,6 +1342,18 @@ def ctx_fused16k(torch_cuda):
     c.close()
 
 
+@pytest.fixture(scope="module")
+def ctx_fused_variants(torch_cuda):
+    """The fused kernel without its XCD-weighted finer split
+    (PRISKV_CRC_FUSED_XW=0: round 3's 16 KiB segments, count split) and
+    without the early first chunks (PRISKV_CRC_FUSED_EARLY=0)."""
+    cs = [_ctx_env(PRISKV_CRC_SEG_MAX_EXTENTS=16384, PRISKV_CRC_FUSED_XW=0),
+          _ctx_env(PRISKV_CRC_SEG_MAX_EXTENTS=16384, PRISKV_CRC_FUSED_EARLY=0)]
+    yield cs
+    for c in cs:
+        c.close()
+
+
 _FUSED_CASES = [
     [256 << 20],                                  # a lone huge value: every workgroup holds part of it
     [(1 << 14) + 1],                              # two segments, the last one byte
@@ -1359,7 +1371,7 @@ _FUSED_CASES = [
 
 
 @pytest.mark.parametrize("case", range(len(_FUSED_CASES) + 2))
-def test_fused_few_extents(torch_cuda, ctx_fused16k, ctx_threelaunch, case):
+def test_fused_few_extents(torch_cuda, ctx_fused16k, ctx_threelaunch, ctx_fused_variants, case):
     """The one-launch few-extents kernel (plan in LDS, per-extent counters,
     last-arriver combine) equals the oracle and the three-launch path, at
     ragged offsets on a 16-B-misaligned base, called repeatedly (the counters
@@ -1386,7 +1398,7 @@ def test_fused_few_extents(torch_cuda, ctx_fused16k, ctx_threelaunch, case):
     d_o = torch.from_numpy(o.astype(np.int64)).cuda()
     d_l = torch.from_numpy(lens.view(np.int32)).cuda()
     want = O.crc32_ranges(base[:n].cpu().numpy(), o, lens)
-    for c in (ctx_fused16k, ctx_threelaunch):
+    for c in [ctx_fused16k, ctx_threelaunch] + ctx_fused_variants:
         for _ in range(3):
             got = _u32(c.ranges_dev(base, d_o, d_l))
             torch.cuda.synchronize()
