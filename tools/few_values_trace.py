@@ -22,6 +22,11 @@ if "--ab" in sys.argv:
     os.environ["PRISKV_CRC_FUSED"] = "0"
     ctxs.append(("three-launch", CrcContext(0)))
     del os.environ["PRISKV_CRC_FUSED"]
+if "--fused-ab" in sys.argv:  # the fused kernel's round-4 options, each off
+    for var in ("PRISKV_CRC_FUSED_XW", "PRISKV_CRC_FUSED_EARLY"):
+        os.environ[var] = "0"
+        ctxs.append((var.split("_")[-1].lower() + "=0", CrcContext(0)))
+        del os.environ[var]
 if "--noseg" in sys.argv:
     os.environ["PRISKV_CRC_SEG_MAX_EXTENTS"] = "0"
     ctxs.append(("unsegmented", CrcContext(0)))
@@ -30,7 +35,9 @@ ctx = ctxs[0][1]
 s = torch.cuda.Stream()
 t = torch.empty(1 << 30, dtype=torch.uint8, device="cuda")
 ctx.fill_splitmix(t, 7, 0)
-for name, n, ln, stride in (("1x256MiB", 1, 256 << 20, 0), ("32x1MiB", 32, 1 << 20, (1 << 20) + 4096),
+ROUNDS = int(next((a.split("=", 1)[1] for a in sys.argv if a.startswith("--rounds=")), "1"))  # whole sweeps
+case_no = 0
+for name, n, ln, stride in ROUNDS * (("1x256MiB", 1, 256 << 20, 0), ("32x1MiB", 32, 1 << 20, (1 << 20) + 4096),
                             ("4096x4KiB-100", 4096, 4096 - 100, 4096), ("4096x64KiB", 4096, 65536, 65536),
                             ("16384x16KiB", 16384, 16384, 16384), ("1x4KiB", 1, 4096, 0), ("64x4KiB", 64, 4096, 4096),
                             ("65x4KiB", 65, 4096, 4096), ("4x64MiB", 4, 64 << 20, 64 << 20),
@@ -38,7 +45,8 @@ for name, n, ln, stride in (("1x256MiB", 1, 256 << 20, 0), ("32x1MiB", 32, 1 << 
     offs = torch.arange(n, dtype=torch.int64, device="cuda") * stride
     lens = torch.full((n,), ln, dtype=torch.int32, device="cuda")
     out = torch.empty(n, dtype=torch.int32, device="cuda")
-    for path, c in ctxs:
+    case_no += 1
+    for path, c in ctxs[case_no % len(ctxs):] + ctxs[:case_no % len(ctxs)]:  # order rotated per case
         with torch.cuda.stream(s):
             for _ in range(30):
                 c.ranges_dev(t, offs, lens, out=out, stream=s)
