@@ -72,7 +72,6 @@ struct priskv_crc_ctx {
     int split;                 // rows kernel split mode for few blocks per wave (PRISKV_CRC_SPLIT=0: off)
     int prio;                  // rows kernel progress priority (PRISKV_CRC_PRIO=0: off)
     int balance;               // byte-balanced extents split (PRISKV_CRC_BALANCE=0: off)
-    int ext_adapt;             // per-wave chunk size of the many-extents shape (PRISKV_CRC_EXT_ADAPT=0: 2 rows)
     int head_split;            // rows kernel + head terms for B = h + whole KiB rows (PRISKV_CRC_HEADSPLIT=0: off)
     uint64_t seg_max_extents;  // device-resident lengths: segment calls of at most this many extents
     int xcd_rr;                // the XCD probe found workgroup b on XCD b % 8 (weights apply)
@@ -336,10 +335,8 @@ int launch_ext_kernel(const priskv_crc_ctx *ctx, bool seg, bool many, bool bal, 
         fn = reinterpret_cast<const void *>(&crc_ranges_kernel<kExtRows, kNbuf, kAux, kExtOpt | 4>);
     else if (bal && !many)
         fn = reinterpret_cast<const void *>(&crc_ranges_kernel<kExtRows, kNbuf, kAux, kExtOpt | 2048>);
-    else if (many && ctx->ext_adapt)
+    else if (many) // 2-row chunks in every wave: 3-12 % slower on scattered values (profiles/r03/ranges/)
         fn = reinterpret_cast<const void *>(&crc_ranges_kernel<kExtRows, kNbuf, kAux, kExtOptMany>);
-    else if (many)
-        fn = reinterpret_cast<const void *>(&crc_ranges_kernel<kExtRows, kNbuf, kAux, kExtOptMany & ~16384>);
     else
         fn = reinterpret_cast<const void *>(&crc_ranges_kernel<kExtRows, kNbuf, kAux, kExtOpt>);
     return herr(hipLaunchKernel(fn, dim3(grid ? grid : 1), dim3(64 * waves), args, 0, s));
@@ -1360,8 +1357,6 @@ int priskv_crc_ctx_create(int device, priskv_crc_ctx **out)
         c->prio = !(pe && !strcmp(pe, "0"));
         const char *be = getenv("PRISKV_CRC_BALANCE");
         c->balance = !(be && !strcmp(be, "0"));
-        const char *ea = getenv("PRISKV_CRC_EXT_ADAPT");
-        c->ext_adapt = !(ea && !strcmp(ea, "0"));
         const char *hs = getenv("PRISKV_CRC_HEADSPLIT");
         c->head_split = !(hs && !strcmp(hs, "0"));
         const char *sb = getenv("PRISKV_CRC_SMALL_BF");
