@@ -185,7 +185,9 @@ int priskv_crc_fill_splitmix_dev(const priskv_crc_ctx *ctx, void *d_dst, uint64_
  * larger such blocks, and every block beyond 64 MiB), 4 = generic (blocks
  * below 16 B: one thread per block), 6 = head split (a multiple of 4 that is
  * whole KiB rows plus a 4-64 B head, 4-byte aligned base: the rows kernel on
- * the bodies, then the heads' terms).  Context options (PRISKV_CRC_STRIDE=0,
+ * the bodies, then the heads' terms; not for a batch of few blocks with
+ * bodies of 64 KiB and more, which the extents path segments -- judged for a
+ * 256-CU device).  Context options (PRISKV_CRC_STRIDE=0,
  * PRISKV_CRC_STRIDE_MAX_KIB) move the 5 / 2 boundary; the exact kernels a
  * given context launches, few-block segmentation included, are reported by
  * priskv_crc32_blocks_plan.  For tests and benchmarks; -EINVAL for invalid
