@@ -1294,11 +1294,15 @@ int priskv_crc_read_roof_dev(const priskv_crc_ctx *ctx, const void *d_base, uint
     if (!g.ok)
         return -ENODEV;
     // the plan the CRC kernel uses for this block size: its pipeline depth,
-    // its resident workgroups and its XCD weights (only with many blocks per
-    // wave, as launch_plan applies them)
+    // its resident workgroups, its split mode (units of block_size / S) and
+    // its XCD weights (only with many units per wave, as launch_plan applies
+    // them); the roof reads units as blocks
     const int p = plan_for(block_size);
     const Plan &P = kPlans[p];
     const uint64_t max_wgs = (uint64_t)ctx->num_cus * ctx->plan_wgs_per_cu[p];
+    const uint32_t S = segments_for(ctx, nblocks, block_size) == 1 ? split_for(ctx, nblocks, block_size) : 1u;
+    block_size /= S;
+    nblocks *= S;
     const uint64_t cps = block_size / 4096;
     const uint64_t cap = max_wgs * kWaves * ((1ull << 31) / cps - 1);
     const uint8_t *base = static_cast<const uint8_t *>(d_base);
@@ -1309,10 +1313,11 @@ int priskv_crc_read_roof_dev(const priskv_crc_ctx *ctx, const void *d_base, uint
         const uint64_t want = (n + kWaves - 1) / kWaves;
         const uint32_t grid = (uint32_t)(want < max_wgs ? want : max_wgs);
         const uint8_t *b = base + done * (uint64_t)block_size;
-        uint32_t *o = d_sink + done;
+        uint32_t *o = d_sink + done / S;
         uint32_t bs = block_size;
         uint32_t xw = n >= 32ull * grid * kWaves ? ctx->plan_xw[p] : 0u;
-        void *args[] = {(void *)&b, (void *)&n, (void *)&bs, (void *)&o, (void *)&xw};
+        uint32_t ush = (uint32_t)log2u(S);
+        void *args[] = {(void *)&b, (void *)&n, (void *)&bs, (void *)&o, (void *)&xw, (void *)&ush};
         if (int rc = herr(hipLaunchKernel(fn, dim3(grid), dim3(kThreads), args, 0, (hipStream_t)stream)))
             return rc;
         done += n;

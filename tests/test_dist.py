@@ -82,3 +82,79 @@ def test_gloo_world2_shard_and_gather(nblocks):
     for rank, allc, t in res:
         assert np.array_equal(allc, want), rank
         assert t == 1.5  # max over ranks of 0.5 + rank
+
+
+def _bench_worker(rank, world, port, fail_ranks, q):
+    try:
+        _bench_worker_body(rank, world, port, fail_ranks, q)
+    except BaseException as e:  # report instead of leaving the test to time out
+        q.put((rank, "error", repr(e), None, None, None, None, None))
+        raise
+
+
+def _bench_worker_body(rank, world, port, fail_ranks, q):
+    """bench.py's Bench collectives at world 8 on CPU (gloo): the allocation
+    agreement with some ranks failing, all_ok, max over ranks and the
+    device-identity gather pair up in the order every leg issues them."""
+    import sys as _sys
+
+    import torch
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    _sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+
+    class _Torch:  # torch with an allocator that fails on the chosen ranks (the tib leg's OOM)
+        OutOfMemoryError = torch.OutOfMemoryError
+        uint8 = torch.uint8
+
+        @staticmethod
+        def empty(n, dtype=None, device=None):
+            if rank in fail_ranks:
+                raise torch.OutOfMemoryError("simulated: cannot allocate")
+            return torch.empty(n, dtype=dtype, device=device)
+
+        class cuda:
+            @staticmethod
+            def empty_cache():
+                pass
+
+    B = bench.Bench(None, _Torch, dist, world, rank, "cpu", None)
+    region, err = B.alloc(1 << 10)           # any failing rank: None everywhere
+    ok_all = B.all_ok(True)
+    ok_one = B.all_ok(rank != 3)
+    mx = B.max(float(rank) * 0.25)
+    infos = bench.gather_obj({"rank": rank}, world)
+    region2, err2 = bench.Bench(None, torch, dist, world, rank, "cpu", None).alloc(1 << 10)  # none fail
+    B.barrier()
+    q.put((rank, region is None, err, ok_all, ok_one, mx, [i["rank"] for i in infos], region2 is not None))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("fail_ranks", [(2, 5), (), (7,)])
+def test_gloo_world8_bench_collectives(fail_ranks):
+    """The N = 8 rehearsal of bench.py's per-leg collectives on CPU: every
+    rank reaches the same decisions (skip on any rank's allocation failure,
+    all_ok false when one rank fails) and the collectives pair up."""
+    world = 8
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_bench_worker, args=(r, world, port, fail_ranks, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted((q.get(timeout=240) for _ in range(world)), key=lambda r: r[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, skipped, err, ok_all, ok_one, mx, ranks, alloc2 in res:
+        assert skipped != "error", (rank, err)
+        assert skipped == bool(fail_ranks), (rank, err)
+        if fail_ranks and rank not in fail_ranks:
+            assert err == "another rank could not allocate"
+        assert ok_all and not ok_one
+        assert mx == 1.75
+        assert ranks == list(range(world))
+        assert alloc2
