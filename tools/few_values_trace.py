@@ -63,14 +63,16 @@ if "--blocks" in sys.argv:  # the rows machinery on 256 MiB: one block (segments
     for bs, nb in ((256 << 20, 1), (64 << 20, 4), (16 << 20, 16), (1 << 20, 1024), (16384, 16384), (4096, 65536),
                    (65536, 4096)):
         out = torch.empty(nb, dtype=torch.int32, device="cuda")
-        with torch.cuda.stream(s):
-            for _ in range(30):
-                ctx.blocks_dev(t, bs, out=out, nblocks=nb, stream=s)
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record(s)
-            for _ in range(100):
-                ctx.blocks_dev(t, bs, out=out, nblocks=nb, stream=s)
-            e1.record(s)
-        e1.synchronize()
-        print(json.dumps({"case": "blocks %dx%d" % (nb, bs), "path": "rows",
-                          "us_per_call": round(e0.elapsed_time(e1) / 100 * 1e3, 2)}), flush=True)
+        for path, c in ctxs:
+            with torch.cuda.stream(s):
+                for _ in range(30):
+                    c.blocks_dev(t, bs, out=out, nblocks=nb, stream=s)
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(s)
+                for _ in range(100):
+                    c.blocks_dev(t, bs, out=out, nblocks=nb, stream=s)
+                e1.record(s)
+            e1.synchronize()
+            print(json.dumps({"case": "blocks %dx%d" % (nb, bs), "path": path,
+                              "plan": c.blocks_plan(t.data_ptr(), nb, bs)[:60],
+                              "us_per_call": round(e0.elapsed_time(e1) / 100 * 1e3, 2)}), flush=True)
