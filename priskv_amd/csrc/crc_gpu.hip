@@ -109,7 +109,6 @@ struct priskv_crc_ctx {
     mutable priskv_crc_pool_slot cnt_pool[NPOOL];
     int fused;                 // few extents in one launch (PRISKV_CRC_FUSED=0: the three-launch path)
     int fused_xw;              // fused kernel: XCD-weighted split of finer segments (PRISKV_CRC_FUSED_XW=0: off)
-    int fused_early;           // fused kernel: first chunks before the tables (PRISKV_CRC_FUSED_EARLY=0: off)
     int stride;                // odd block sizes / unaligned bases take crc_stride_kernel (PRISKV_CRC_STRIDE=0: the
                                // extents / generic kernels, as in round 2)
     int stride_g;              // PRISKV_CRC_STRIDE_G: force the stride kernel's G (0 = cost model; tests)
@@ -701,10 +700,7 @@ int launch_fused(const priskv_crc_ctx *ctx, const uint8_t *base, uint64_t n, con
     uint32_t xw = ctx->fused_xw ? ctx->plan_xw[PLAN_4K] : 0u;
     // 2-row chunks: 4 and 8 rows lost 6-13 % on a lone 256 MiB value (profiles/r03/fused/)
     const void *fn =
-        ctx->fused_early
-            ? reinterpret_cast<const void *>(
-                  &crc_ranges_fused_kernel<kExtRows, kNbuf, kAux, kFusedPrio, kFusedWaves, true>)
-            : reinterpret_cast<const void *>(&crc_ranges_fused_kernel<kExtRows, kNbuf, kAux, kFusedPrio, kFusedWaves>);
+        reinterpret_cast<const void *>(&crc_ranges_fused_kernel<kExtRows, kNbuf, kAux, kFusedPrio, kFusedWaves>);
     const uint32_t *img = ctx->d_lds_image[0], *nib = ctx->d_nib16, *rs = ctx->d_rowshift, *zp = ctx->d_zpow;
     void *args[] = {(void *)&abase, (void *)&n,   (void *)&offs, (void *)&lens_or_null, (void *)&sh,
                     (void *)&stride, (void *)&len_const, (void *)&img, (void *)&nib, (void *)&rs,
@@ -1370,8 +1366,6 @@ int priskv_crc_ctx_create(int device, priskv_crc_ctx **out)
         c->fused = !(fe && !strcmp(fe, "0"));
         const char *fx = getenv("PRISKV_CRC_FUSED_XW");
         c->fused_xw = !(fx && !strcmp(fx, "0"));
-        const char *fy = getenv("PRISKV_CRC_FUSED_EARLY");
-        c->fused_early = !(fy && !strcmp(fy, "0"));
         const char *se = getenv("PRISKV_CRC_STRIDE");
         c->stride = !(se && !strcmp(se, "0"));
         c->stride_g = 0;

@@ -1345,10 +1345,8 @@ def ctx_fused16k(torch_cuda):
 @pytest.fixture(scope="module")
 def ctx_fused_variants(torch_cuda):
     """The fused kernel without its XCD-weighted finer split
-    (PRISKV_CRC_FUSED_XW=0: round 3's 16 KiB segments, count split) and
-    without the early first chunks (PRISKV_CRC_FUSED_EARLY=0)."""
-    cs = [_ctx_env(PRISKV_CRC_SEG_MAX_EXTENTS=16384, PRISKV_CRC_FUSED_XW=0),
-          _ctx_env(PRISKV_CRC_SEG_MAX_EXTENTS=16384, PRISKV_CRC_FUSED_EARLY=0)]
+    (PRISKV_CRC_FUSED_XW=0: round 3's 16 KiB segments, count split)."""
+    cs = [_ctx_env(PRISKV_CRC_SEG_MAX_EXTENTS=16384, PRISKV_CRC_FUSED_XW=0)]
     yield cs
     for c in cs:
         c.close()

@@ -23,7 +23,7 @@ if "--ab" in sys.argv:
     ctxs.append(("three-launch", CrcContext(0)))
     del os.environ["PRISKV_CRC_FUSED"]
 if "--fused-ab" in sys.argv:  # the fused kernel's round-4 options, each off
-    for var in ("PRISKV_CRC_FUSED_XW", "PRISKV_CRC_FUSED_EARLY"):
+    for var in ("PRISKV_CRC_FUSED_XW",):
         os.environ[var] = "0"
         ctxs.append((var.split("_")[-1].lower() + "=0", CrcContext(0)))
         del os.environ[var]
