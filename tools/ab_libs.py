@@ -1,14 +1,16 @@
 #!/usr/bin/env python3
-"""A/B of two builds of libpriskv_crc.so in ONE process (tools only).
+"""A/B of library builds and context options in ONE process (tools only).
 
-  python tools/ab_libs.py A.so B.so [rounds]
+  python tools/ab_libs.py VARIANT VARIANT ... [--rounds=R] [--cases=a,b]
 
-Both libraries are loaded side by side (ctypes, RTLD_LOCAL: separate symbol
-namespaces), each with its own context on device 0; every case is timed with
-HIP events over back-to-back calls on one stream, the two libraries
-alternating (order rotated per round), on the same device buffers.  Prints
-one JSON line per (round, case, library).  Used for kernel changes that have
-no runtime switch (round 4: the fused kernel's wave plan before its tables).
+VARIANT = path/to/libpriskv_crc.so[@VAR=V+VAR=V]: the library (loaded with
+ctypes, RTLD_LOCAL: two builds keep separate symbol namespaces) and the
+PRISKV_CRC_* environment its context is created with.  Every case is timed
+with HIP events over back-to-back calls on one stream, the variants
+alternating (order rotated per case and round), on the same device buffers,
+and every variant's CRCs must agree bit for bit.  One JSON line per (round,
+case, variant).  For kernel changes without a runtime switch (round 4: the
+fused kernel's wave plan before its tables) and for tuning switches.
 """
 import ctypes
 import json
@@ -17,12 +19,17 @@ import sys
 
 import torch
 
-A, B = sys.argv[1], sys.argv[2]
-ROUNDS = int(sys.argv[3]) if len(sys.argv) > 3 else 3
+ARGS = [a for a in sys.argv[1:] if not a.startswith("--")]
+ROUNDS = int(next((a.split("=", 1)[1] for a in sys.argv if a.startswith("--rounds=")), "3"))
+ONLY = next((a.split("=", 1)[1].split(",") for a in sys.argv if a.startswith("--cases=")), None)
 C = ctypes
 
 
-def load(path):
+def load(spec):
+    path, _, env = spec.partition("@")
+    kv = [e.split("=", 1) for e in env.split("+") if e]
+    for k, v in kv:
+        os.environ[k] = v
     L = C.CDLL(os.path.abspath(path))
     L.priskv_crc_ctx_create.argtypes = [C.c_int, C.POINTER(C.c_void_p)]
     L.priskv_crc32_ranges_dev.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p,
@@ -30,10 +37,13 @@ def load(path):
     L.priskv_crc32_blocks_dev.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint32, C.c_void_p, C.c_void_p]
     h = C.c_void_p()
     assert L.priskv_crc_ctx_create(0, C.byref(h)) == 0
+    for k, _ in kv:
+        del os.environ[k]
     return L, h
 
 
-libs = {"A": load(A), "B": load(B)}
+libs = {a: load(a) for a in ARGS}
+TAGS = list(libs)
 s = torch.cuda.Stream()
 region = torch.empty(1 << 30, dtype=torch.uint8, device="cuda")
 g = torch.Generator(device="cuda").manual_seed(7)
@@ -48,7 +58,10 @@ for r in range(ROUNDS):
         offs = torch.arange(n, dtype=torch.int64, device="cuda") * stride
         lens = torch.full((n,), ln, dtype=torch.int32, device="cuda")
         out = torch.empty(n, dtype=torch.int32, device="cuda")
-        order = ["A", "B"] if (r + ci) % 2 == 0 else ["B", "A"]
+        if ONLY and not any(o in name for o in ONLY):
+            continue
+        k = (r + ci) % len(TAGS)
+        order = TAGS[k:] + TAGS[:k]
         for tag in order:
             L, h = libs[tag]
             sp = s.cuda_stream
@@ -70,5 +83,5 @@ for r in range(ROUNDS):
             e1.synchronize()
             got = out.cpu().numpy().tobytes()
             assert ref.setdefault(name, got) == got, (name, tag)  # A and B agree bit for bit
-            print(json.dumps({"round": r, "case": name, "lib": tag, "us_per_call": round(e0.elapsed_time(e1) / 50 * 1e3, 2)}),
+            print(json.dumps({"round": r, "case": name, "variant": tag, "us_per_call": round(e0.elapsed_time(e1) / 50 * 1e3, 2)}),
                   flush=True)
