@@ -109,7 +109,6 @@ struct priskv_crc_ctx {
     mutable priskv_crc_pool_slot cnt_pool[NPOOL];
     int fused;                 // few extents in one launch (PRISKV_CRC_FUSED=0: the three-launch path)
     int fused_xw;              // fused kernel: XCD-weighted split of finer segments (PRISKV_CRC_FUSED_XW=0: off)
-    int fused_shape;           // fused kernel waves / chunk shape (PRISKV_CRC_FUSED_SHAPE; tuning)
     int stride;                // odd block sizes / unaligned bases take crc_stride_kernel (PRISKV_CRC_STRIDE=0: the
                                // extents / generic kernels, as in round 2)
     int stride_g;              // PRISKV_CRC_STRIDE_G: force the stride kernel's G (0 = cost model; tests)
@@ -652,6 +651,7 @@ constexpr uint32_t kSegMinLen = 64u << 10;
 constexpr int kFusedPrio = 0;
 constexpr uint64_t kFusedUnitsPerWave = 32; // with XCD weights (fused_xw)
 constexpr uint32_t kFusedMinShift = 10;     // ... segments of at least 1 KiB
+constexpr uint64_t kFusedFewExtents = 16;   // the 8-wave shape up to this many extents
 
 // one segment size per call (crc_seg_plan_kernel / the fused kernel): about
 // kSegPerWave full segments per resident wave, so the count split of
@@ -694,21 +694,22 @@ int launch_fused(const priskv_crc_ctx *ctx, const uint8_t *base, uint64_t n, con
     // XCD weights (fused_xw): segments of >= 1 KiB, about kFusedUnitsPerWave per
     // resident wave, so that the weights (whole units) apply to large calls;
     // else about kSegPerWave of >= 16 KiB (round 3)
-    // shape (PRISKV_CRC_FUSED_SHAPE, tuning): 0 = 16 waves x 2-row chunks x 2
-    // deep; 1 = 8 waves x 2 x 2; 2 = 8 waves x 4 x 3; 3 = 8 waves x 4 x 2
-    const int nw = ctx->fused_shape ? 8 : kFusedWaves;
+    // Shape: 16 waves per CU with 2-row chunks 2 deep; for at most
+    // kFusedFewExtents extents -- a lone large value, a few: the ones with
+    // the most bytes per wave -- 8 waves with 4-row chunks 2 deep (the 64 KiB
+    // rows plan's), which stream 4-8 % faster there but lose 7 % at 32 x 1 MiB
+    // (profiles/r04/fused/shape_ab.jsonl; 8 x 2 x 2 and 8 x 4 x 3 lost).
+    const bool few = n <= kFusedFewExtents;
+    const int nw = few ? 8 : kFusedWaves;
     const uint64_t waves = (uint64_t)ctx->num_cus * nw;
     const uint64_t want = ctx->fused_xw ? kFusedUnitsPerWave * waves : seg_target(ctx);
     const uint32_t tgt = 1u << (31 - __builtin_clz((uint32_t)std::min<uint64_t>(want, 1u << 30))); // a power of two
     uint32_t ms = ctx->fused_xw ? kFusedMinShift : kSegMinShift;
     uint32_t xw = ctx->fused_xw ? ctx->plan_xw[PLAN_4K] : 0u;
-    // 2-row chunks: 4 and 8 rows lost 6-13 % on a lone 256 MiB value (profiles/r03/fused/)
+    // (16 waves: 4- and 8-row chunks lost 6-13 % on a lone 256 MiB value, profiles/r03/fused/)
     const void *fn =
-        ctx->fused_shape == 1   ? reinterpret_cast<const void *>(&crc_ranges_fused_kernel<2, 2, kAux, kFusedPrio, 8>)
-        : ctx->fused_shape == 2 ? reinterpret_cast<const void *>(&crc_ranges_fused_kernel<4, 3, kAux, kFusedPrio, 8>)
-        : ctx->fused_shape == 3 ? reinterpret_cast<const void *>(&crc_ranges_fused_kernel<4, 2, kAux, kFusedPrio, 8>)
-                                : reinterpret_cast<const void *>(
-                                      &crc_ranges_fused_kernel<kExtRows, kNbuf, kAux, kFusedPrio, kFusedWaves>);
+        few ? reinterpret_cast<const void *>(&crc_ranges_fused_kernel<4, kNbuf, kAux, kFusedPrio, 8>)
+            : reinterpret_cast<const void *>(&crc_ranges_fused_kernel<kExtRows, kNbuf, kAux, kFusedPrio, kFusedWaves>);
     const uint32_t *img = ctx->d_lds_image[0], *nib = ctx->d_nib16, *rs = ctx->d_rowshift, *zp = ctx->d_zpow;
     void *args[] = {(void *)&abase, (void *)&n,   (void *)&offs, (void *)&lens_or_null, (void *)&sh,
                     (void *)&stride, (void *)&len_const, (void *)&img, (void *)&nib, (void *)&rs,
@@ -1374,8 +1375,6 @@ int priskv_crc_ctx_create(int device, priskv_crc_ctx **out)
         c->fused = !(fe && !strcmp(fe, "0"));
         const char *fx = getenv("PRISKV_CRC_FUSED_XW");
         c->fused_xw = !(fx && !strcmp(fx, "0"));
-        const char *fsh = getenv("PRISKV_CRC_FUSED_SHAPE");
-        c->fused_shape = fsh ? (atoi(fsh) & 3) : 0;
         const char *se = getenv("PRISKV_CRC_STRIDE");
         c->stride = !(se && !strcmp(se, "0"));
         c->stride_g = 0;
