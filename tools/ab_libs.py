@@ -51,7 +51,8 @@ region.random_(0, 256, generator=g)
 CASES = [("ranges 1x256MiB", 1, 256 << 20, 0), ("ranges 32x1MiB", 32, 1 << 20, (1 << 20) + 4096),
          ("ranges 4x64MiB", 4, 64 << 20, 64 << 20), ("ranges 1024x1MiB", 1024, 1 << 20, 1 << 20),
          ("ranges 65x4KiB", 65, 4096, 4096), ("ranges 4096x64KiB", 4096, 65536, 65536),
-         ("blocks 1x256MiB", 1, 256 << 20, 0), ("blocks 16x16MiB", 16, 16 << 20, 0)]
+         ("blocks 1x256MiB", 1, 256 << 20, 0), ("blocks 16x16MiB", 16, 16 << 20, 0),
+         ("blocks 65536x4KiB", 65536, 4096, 0), ("blocks 4096x64KiB", 4096, 65536, 0)]
 ref = {}
 for r in range(ROUNDS):
     for ci, (name, n, ln, stride) in enumerate(CASES):
