@@ -45,7 +45,7 @@ def load(spec):
 libs = {a: load(a) for a in ARGS}
 TAGS = list(libs)
 s = torch.cuda.Stream()
-region = torch.empty(1 << 30, dtype=torch.uint8, device="cuda")
+region = torch.empty(4 << 30, dtype=torch.uint8, device="cuda")
 g = torch.Generator(device="cuda").manual_seed(7)
 region.random_(0, 256, generator=g)
 CASES = [("ranges 1x256MiB", 1, 256 << 20, 0), ("ranges 32x1MiB", 32, 1 << 20, (1 << 20) + 4096),
@@ -53,11 +53,27 @@ CASES = [("ranges 1x256MiB", 1, 256 << 20, 0), ("ranges 32x1MiB", 32, 1 << 20, (
          ("ranges 65x4KiB", 65, 4096, 4096), ("ranges 4096x64KiB", 4096, 65536, 65536),
          ("blocks 1x256MiB", 1, 256 << 20, 0), ("blocks 16x16MiB", 16, 16 << 20, 0),
          ("blocks 65536x4KiB", 65536, 4096, 0), ("blocks 4096x64KiB", 4096, 65536, 0)]
+# PrisKV-shaped scattered values (tools/values_bench.py extents(): 1-4 blocks,
+# ragged ends, random blocks of the region)
+import numpy as np  # noqa: E402
+_rng = np.random.default_rng(1)
+SCATTER = {}
+for _name, _bs, _n in (("priskv4k", 4096, 1 << 19), ("priskv64k", 65536, 1 << 15)):
+    _k = _rng.integers(0, 3, _n)
+    _span = (1 << _k) * _bs
+    _blk = _rng.integers(0, region.numel() // _bs - 4, _n)
+    _o = (_blk * _bs).astype(np.uint64)
+    _l = np.minimum(_span - _rng.integers(0, _bs, _n), region.numel() - _o).astype(np.uint32)
+    SCATTER[_name] = (torch.from_numpy(_o.astype(np.int64)).cuda(), torch.from_numpy(_l.view(np.int32)).cuda())
+    CASES.append(("ranges " + _name, _n, 0, 0))
 ref = {}
 for r in range(ROUNDS):
     for ci, (name, n, ln, stride) in enumerate(CASES):
-        offs = torch.arange(n, dtype=torch.int64, device="cuda") * stride
-        lens = torch.full((n,), ln, dtype=torch.int32, device="cuda")
+        if name.split()[-1] in SCATTER:
+            offs, lens = SCATTER[name.split()[-1]]
+        else:
+            offs = torch.arange(n, dtype=torch.int64, device="cuda") * stride
+            lens = torch.full((n,), ln, dtype=torch.int32, device="cuda")
         out = torch.empty(n, dtype=torch.int32, device="cuda")
         if ONLY and not any(o in name for o in ONLY):
             continue
