@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """A/B of library builds and context options in ONE process (tools only).
 
-  python tools/ab_libs.py VARIANT VARIANT ... [--rounds=R] [--cases=a,b]
+  python tools/ab_libs.py VARIANT VARIANT ... [--rounds=R] [--cases=a+b]
 
 VARIANT = path/to/libpriskv_crc.so[@VAR=V+VAR=V]: the library (loaded with
 ctypes, RTLD_LOCAL: two builds keep separate symbol namespaces) and the
@@ -21,7 +21,7 @@ import torch
 
 ARGS = [a for a in sys.argv[1:] if not a.startswith("--")]
 ROUNDS = int(next((a.split("=", 1)[1] for a in sys.argv if a.startswith("--rounds=")), "3"))
-ONLY = next((a.split("=", 1)[1].split(",") for a in sys.argv if a.startswith("--cases=")), None)
+ONLY = next((a.split("=", 1)[1].split("+") for a in sys.argv if a.startswith("--cases=")), None)
 C = ctypes
 
 
