@@ -707,12 +707,9 @@ int launch_fused(const priskv_crc_ctx *ctx, const uint8_t *base, uint64_t n, con
     uint32_t ms = ctx->fused_xw ? kFusedMinShift : kSegMinShift;
     uint32_t xw = ctx->fused_xw ? ctx->plan_xw[PLAN_4K] : 0u;
     // (16 waves: 4- and 8-row chunks lost 6-13 % on a lone 256 MiB value, profiles/r03/fused/)
-    static const int tune = getenv("PRISKV_CRC_FUSED_TUNE") ? atoi(getenv("PRISKV_CRC_FUSED_TUNE")) : 0; // A/B only
+    // (8 waves: progress priority, 3-deep 4-row and 2-deep 8-row chunks all level, profiles/r04/fused/prio_depth_ab.jsonl)
     const void *fn =
-        few ? (tune == 1   ? reinterpret_cast<const void *>(&crc_ranges_fused_kernel<4, kNbuf, kAux, 3, 8>)
-               : tune == 2 ? reinterpret_cast<const void *>(&crc_ranges_fused_kernel<4, 3, kAux, 3, 8>)
-               : tune == 3 ? reinterpret_cast<const void *>(&crc_ranges_fused_kernel<8, kNbuf, kAux, 0, 8>)
-                           : reinterpret_cast<const void *>(&crc_ranges_fused_kernel<4, kNbuf, kAux, kFusedPrio, 8>))
+        few ? reinterpret_cast<const void *>(&crc_ranges_fused_kernel<4, kNbuf, kAux, kFusedPrio, 8>)
             : reinterpret_cast<const void *>(&crc_ranges_fused_kernel<kExtRows, kNbuf, kAux, kFusedPrio, kFusedWaves>);
     const uint32_t *img = ctx->d_lds_image[0], *nib = ctx->d_nib16, *rs = ctx->d_rowshift, *zp = ctx->d_zpow;
     void *args[] = {(void *)&abase, (void *)&n,   (void *)&offs, (void *)&lens_or_null, (void *)&sh,
