@@ -66,8 +66,8 @@ struct priskv_crc_ctx {
     int device;
     int num_cus;
     int max_wgs;               // resident workgroups of the sub-KiB kernel (2 per CU)
-    int plan_wgs_per_cu[8];    // resident workgroups per CU of each rows-kernel plan
-    uint32_t plan_xw[8];       // rows-kernel split per plan: (even << 16) | odd XCD weight, 0 = equal
+    int plan_wgs_per_cu[16];   // resident workgroups per CU of each rows-kernel plan
+    uint32_t plan_xw[16];      // rows-kernel split per plan: (even << 16) | odd XCD weight, 0 = equal
     int segment;               // split few large blocks / extents into segments (PRISKV_CRC_SEGMENT=0: off)
     int split;                 // rows kernel split mode for few blocks per wave (PRISKV_CRC_SPLIT=0: off)
     int prio;                  // rows kernel progress priority (PRISKV_CRC_PRIO=0: off)
@@ -398,9 +398,10 @@ enum PlanId {
     PLAN_G64_CH4_BIG,  // 256 KiB and up (multiples of 4 KiB)
     PLAN_G64_CH2,
     PLAN_G64_CH1,
+    PLAN_SPLIT_DEEP,   // split mode for few large blocks: G64, CH4, 3 chunks in flight, first chunks before the tables
     NPLANS
 };
-static_assert(NPLANS <= 8, "priskv_crc_ctx per-plan arrays");
+static_assert(NPLANS <= 16, "priskv_crc_ctx per-plan arrays");
 struct Plan {
     int G, CH, NBUF, opt, wg_per_cu;
     uint32_t we, wo; // even:odd XCD weights of the static split
@@ -425,7 +426,8 @@ constexpr int kPrio1 = 1 << 8, kPrio3 = 3 << 8, kEarly = 16;
 constexpr Plan kPlans[NPLANS] = {
     {64, 4, 3, 2 | kEarly | 32 | kPrio3, 1, 31, 29}, {64, 4, 2, 32 | kPrio1, 1, 31, 29}, {16, 4, 2, 2 | 32 | kPrio1, 1, 31, 29},
     {16, 4, 2, kPrio1, 1, 31, 29},          {64, 4, 2, kPrio1, 1, 31, 29},      {64, 4, 2, kPrio3, 1, 31, 29},
-    {64, 2, 2, 0, 1, 31, 29},               {64, 1, 2, 0, 1, 31, 29}};
+    {64, 2, 2, 0, 1, 31, 29},               {64, 1, 2, 0, 1, 31, 29},
+    {64, 4, 3, kEarly | 32 | kPrio3, 1, 31, 29}};
 
 int plan_for(uint32_t bs)
 {
@@ -480,6 +482,7 @@ const void *plan_fn(int p, bool prio, bool split = false)
     case PLAN_G64_CH4: return plan_kernel_p<PLAN_G64_CH4>(prio, split);
     case PLAN_G64_CH4_BIG: return plan_kernel_p<PLAN_G64_CH4_BIG>(prio, split);
     case PLAN_G64_CH2: return plan_kernel_p<PLAN_G64_CH2>(prio, split);
+    case PLAN_SPLIT_DEEP: return plan_kernel_p<PLAN_SPLIT_DEEP>(prio, split);
     default: return plan_kernel_p<PLAN_G64_CH1>(prio, split);
     }
 }
@@ -608,14 +611,31 @@ uint32_t split_for(const priskv_crc_ctx *ctx, uint64_t nblocks, uint32_t bs)
     return nblocks * S >= want ? S : 1;
 }
 
-int launch_split(const priskv_crc_ctx *ctx, const uint8_t *base, uint64_t nblocks, uint32_t bs, uint32_t S,
+// Few large blocks (the count split is unbalanced, segments_for > 1): the
+// same split mode instead of segments + a combine kernel or the fused
+// kernel, with units down to one 4 KiB chunk, and on the 3-deep plan that
+// requests its first chunks before the tables (the 4 KiB plan's edge at
+// small calls: DESIGN §6).  1 = not applicable (then segments as before).
+uint32_t split_few(const priskv_crc_ctx *ctx, uint64_t nblocks, uint32_t bs)
+{
+    if (!ctx->split || bs % 4096 != 0)
+        return 1;
+    const uint64_t want =
+        kSplitUnitsPerWave * (uint64_t)ctx->num_cus * ctx->plan_wgs_per_cu[PLAN_SPLIT_DEEP] * kWaves;
+    uint32_t S = 1;
+    while (nblocks * S < want && (bs / 4096) % (2 * S) == 0)
+        S *= 2;
+    return nblocks * S >= want ? S : 1;
+}
+
+int launch_split(const priskv_crc_ctx *ctx, int p, const uint8_t *base, uint64_t nblocks, uint32_t bs, uint32_t S,
                  uint32_t *out, hipStream_t s)
 {
     Scratch sc(ctx, s, ctx->cnt_pool, true); // zero at rest: the kernel leaves it zero
     if (int rc = sc.get((size_t)nblocks * 8))
         return rc;
     uint32_t *cnt = static_cast<uint32_t *>(sc.p);
-    const int rc = launch_plan(ctx, plan_for(bs), base, nblocks, bs, out, s, 0, S, cnt, cnt + nblocks);
+    const int rc = launch_plan(ctx, p, base, nblocks, bs, out, s, 0, S, cnt, cnt + nblocks);
     const int frc = sc.release();
     return rc ? rc : frc;
 }
@@ -771,9 +791,11 @@ int launch_rows(const priskv_crc_ctx *ctx, const uint8_t *base, uint64_t nblocks
     const uint32_t S = segments_for(ctx, nblocks, bs);
     if (S == 1) {
         const uint32_t sp = split_for(ctx, nblocks, bs);
-        return sp > 1 ? launch_split(ctx, base, nblocks, bs, sp, out, s)
+        return sp > 1 ? launch_split(ctx, plan_for(bs), base, nblocks, bs, sp, out, s)
                       : launch_rows_plain(ctx, base, nblocks, bs, out, s);
     }
+    if (const uint32_t sf = split_few(ctx, nblocks, bs); sf > 1)
+        return launch_split(ctx, PLAN_SPLIT_DEEP, base, nblocks, bs, sf, out, s);
     // few large blocks: the fused few-extents kernel in one launch (1 x 256 MiB
     // 50 us against 55-57 for rows + combine, 1024 x 1 MiB level: DESIGN §4)
     if (fused_blocks(ctx, nblocks))
@@ -1245,6 +1267,17 @@ int priskv_crc32_blocks_plan(const priskv_crc_ctx *ctx, const void *d_base, uint
                          P.G, ch, nbuf, bf ? ",byte-fold" : "", pm ? ",progress-priority 3" : "", P.R, 16u * P.G,
                          P.R * 16u * P.G - block_size);
         }
+    } else if (path == PATH_ROWS && segments_for(ctx, nblocks, block_size) > 1 &&
+               split_few(ctx, nblocks, block_size) > 1) {
+        const uint32_t sf = split_few(ctx, nblocks, block_size), xw = ctx->plan_xw[PLAN_SPLIT_DEEP];
+        w = snprintf(buf, len,
+                     "crc_rows_kernel<G=64,CH=4,NBUF=3,nt,nibble-fold%s,first chunks before the tables,"
+                     "split %u units of %u B per block%s",
+                     ctx->prio ? ",progress-priority 3" : "", sf, block_size / sf, xw ? ",xcd-weighted" : "");
+        if (w >= 0 && (uint64_t)w < len && xw)
+            w += snprintf(buf + w, len - w, " %u:%u", xw >> 16, xw & 0xFFFF);
+        if (w >= 0 && (uint64_t)w < len)
+            w += snprintf(buf + w, len - w, "> (few large blocks)");
     } else if (path == PATH_ROWS && segments_for(ctx, nblocks, block_size) > 1 && fused_blocks(ctx, nblocks)) {
         w = snprintf(buf, len, "%s", fused_name);
     } else if (path == PATH_ROWS || path == PATH_HEAD) {
@@ -1303,10 +1336,14 @@ int priskv_crc_read_roof_dev(const priskv_crc_ctx *ctx, const void *d_base, uint
     // its resident workgroups, its split mode (units of block_size / S) and
     // its XCD weights (only with many units per wave, as launch_plan applies
     // them); the roof reads units as blocks
-    const int p = plan_for(block_size);
+    int p = plan_for(block_size);
+    uint32_t S = 1;
+    if (segments_for(ctx, nblocks, block_size) == 1)
+        S = split_for(ctx, nblocks, block_size);
+    else if ((S = split_few(ctx, nblocks, block_size)) > 1)
+        p = PLAN_SPLIT_DEEP;
     const Plan &P = kPlans[p];
     const uint64_t max_wgs = (uint64_t)ctx->num_cus * ctx->plan_wgs_per_cu[p];
-    const uint32_t S = segments_for(ctx, nblocks, block_size) == 1 ? split_for(ctx, nblocks, block_size) : 1u;
     block_size /= S;
     nblocks *= S;
     const uint64_t cps = block_size / 4096;

@@ -991,7 +991,9 @@ def test_full_config_1M_x_4K(torch_cuda, ctx):
 # (block size, blocks): balanced batches with few blocks per wave; 1900 x
 # 1 MiB gives fewer units per wave than units per block (waves whose whole
 # range lies inside one block)
-_SPLIT_CASES = [(1 << 20, 1900), (1 << 20, 4096), (512 << 10, 4000), (256 << 10, 6000), (1 << 20, 2048)]
+_SPLIT_CASES = [(1 << 20, 1900), (1 << 20, 4096), (512 << 10, 4000), (256 << 10, 6000), (1 << 20, 2048),
+                # few large blocks: the 3-deep plan, units down to one 4 KiB chunk
+                (256 << 20, 1), (16 << 20, 16), (1 << 20, 1000), (12 << 20, 3)]
 
 
 @pytest.mark.parametrize("bs,nb", _SPLIT_CASES)
@@ -1006,7 +1008,9 @@ def test_rows_split_mode(torch_cuda, ctx, bs, nb):
     view = t[:bs * nb]
     plan = ctx.blocks_plan(view.data_ptr(), nb, bs)
     xcd = "xcd-weighted" in ctx.blocks_plan(view.data_ptr(), 1 << 20, 4096)  # the probe saw round-robin XCDs
-    assert ("split" in plan) == xcd, plan
+    few = nb * 10 < 9 * 2048  # unbalanced: split whether or not the weights apply
+    assert ("split" in plan) == (xcd or few), plan
+    assert ("few large blocks" in plan) == few, plan
     want = O.crc32_blocks(view.cpu().numpy(), bs, nthreads=16)
     off = _ctx_env(PRISKV_CRC_SPLIT=0)
     try:
@@ -1151,8 +1155,12 @@ def test_blocks_plan_strings(torch_cuda, ctx):
     assert ctx.blocks_plan(base, 1, 1 << 20).startswith("crc_ranges_fused_kernel")  # few large blocks
     assert ctx.blocks_plan(base + 1, 3, (3 << 20) + 5).startswith("crc_ranges_fused_kernel")
     assert ctx.blocks_plan(base, 20000, 1 << 20).startswith("crc_rows_kernel")  # balanced: whole blocks
-    # more than 64 unbalanced large blocks: rows kernel on segments + combine
-    assert "crc_combine_segments_kernel" in ctx.blocks_plan(base, 1000, 1 << 20)
+    # unbalanced large blocks that can be cut into 32 units per wave: the
+    # rows kernel's split mode on the 3-deep plan (one launch)
+    assert "few large blocks" in ctx.blocks_plan(base, 1000, 1 << 20)
+    assert "few large blocks" in ctx.blocks_plan(base, 1, 256 << 20)
+    # ... else segments + combine
+    assert "crc_combine_segments_kernel" in ctx.blocks_plan(base, 1000, (1 << 20) + 1024)
     assert ctx.blocks_plan(base, 100, 256) == "crc_small_kernel<G=16,byte-fold>"
     # odd sizes and unaligned bases: the uniform-stride kernel
     assert ctx.blocks_plan(base + 1, 100, 4096).startswith("crc_stride_kernel<G=32,CH=8,NBUF=2,nt,progress-priority 3> (8 rows of 512 B")
@@ -1432,7 +1440,7 @@ def test_fused_single_value_beyond_2GiB(torch_cuda, ctx, kind):
     if kind == "block_3GiB":
         bs = 3 << 30
         t = _region(torch, ctx, bs, SEED ^ 0x3, 0)
-        assert ctx.blocks_plan(t.data_ptr(), 1, bs).startswith("crc_ranges_fused_kernel")
+        assert "few large blocks" in ctx.blocks_plan(t.data_ptr(), 1, bs)  # the rows kernel's split mode
         got = _u32(ctx.blocks_dev(t, bs, nblocks=1))
         torch.cuda.synchronize()
         want = O.crc32_blocks(t[:bs].cpu().numpy(), bs, nthreads=8)
