@@ -993,7 +993,9 @@ def test_full_config_1M_x_4K(torch_cuda, ctx):
 # range lies inside one block)
 _SPLIT_CASES = [(1 << 20, 1900), (1 << 20, 4096), (512 << 10, 4000), (256 << 10, 6000), (1 << 20, 2048),
                 # few large blocks: the 3-deep plan, units down to one 4 KiB chunk
-                (256 << 20, 1), (16 << 20, 16), (1 << 20, 1000), (12 << 20, 3)]
+                (256 << 20, 1), (16 << 20, 16), (1 << 20, 1000), (32 << 20, 8),
+                # ... but not when they cannot be cut into 32 units per wave (the fused kernel)
+                (12 << 20, 3)]
 
 
 @pytest.mark.parametrize("bs,nb", _SPLIT_CASES)
@@ -1008,8 +1010,10 @@ def test_rows_split_mode(torch_cuda, ctx, bs, nb):
     view = t[:bs * nb]
     plan = ctx.blocks_plan(view.data_ptr(), nb, bs)
     xcd = "xcd-weighted" in ctx.blocks_plan(view.data_ptr(), 1 << 20, 4096)  # the probe saw round-robin XCDs
-    few = nb * 10 < 9 * 2048  # unbalanced: split whether or not the weights apply
-    assert ("split" in plan) == (xcd or few), plan
+    waves = torch.cuda.get_device_properties(0).multi_processor_count * 8
+    unbal = nb * 10 < 9 * waves
+    few = unbal and nb * (bs // 4096) >= 32 * waves  # unbalanced and 32 units of >= 4 KiB per wave
+    assert ("split" in plan) == (few or (xcd and not unbal)), plan
     assert ("few large blocks" in plan) == few, plan
     want = O.crc32_blocks(view.cpu().numpy(), bs, nthreads=16)
     off = _ctx_env(PRISKV_CRC_SPLIT=0)
