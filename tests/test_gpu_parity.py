@@ -1164,7 +1164,7 @@ def test_blocks_plan_strings(torch_cuda, ctx):
     assert "few large blocks" in ctx.blocks_plan(base, 1000, 1 << 20)
     assert "few large blocks" in ctx.blocks_plan(base, 1, 256 << 20)
     # ... else segments + combine
-    assert "crc_combine_segments_kernel" in ctx.blocks_plan(base, 1000, (1 << 20) + 1024)
+    assert "crc_combine_segments_kernel" in ctx.blocks_plan(base, 1000, (1 << 20) + 2048)
     assert ctx.blocks_plan(base, 100, 256) == "crc_small_kernel<G=16,byte-fold>"
     # odd sizes and unaligned bases: the uniform-stride kernel
     assert ctx.blocks_plan(base + 1, 100, 4096).startswith("crc_stride_kernel<G=32,CH=8,NBUF=2,nt,progress-priority 3> (8 rows of 512 B")
