@@ -456,7 +456,7 @@ const void *plan_kernel()
 // prio = false: the plan's kernel without progress priority (PRISKV_CRC_PRIO=0);
 // split: its split-mode instance (plans with one block per wave group and an
 // unpipelined fold: plan_splits)
-constexpr int kSplitOpt = 64;
+constexpr int kSplitOpt = 64, kMergeOpt = 128;
 constexpr bool plan_splits(int p) { return kPlans[p].G == 64 && !(kPlans[p].opt & 2); }
 
 template <int P>
@@ -465,9 +465,12 @@ const void *plan_kernel_p(bool prio, bool split)
     constexpr Plan Q = kPlans[P];
     constexpr int O = prio_free(Q.opt);
     if constexpr (plan_splits(P)) {
+        // the few-large-blocks plan merges its parts per workgroup (a lone
+        // block has a part in every wave; per-wave atomics elsewhere: the
+        // workgroup barrier cost 2 % on 4 Ki x 1 MiB, profiles/r04/split/)
+        constexpr int SO = kSplitOpt | (P == PLAN_SPLIT_DEEP ? kMergeOpt : 0);
         if (split)
-            return prio ? plan_kernel<Q.G, Q.CH, Q.NBUF, Q.opt | kSplitOpt>()
-                        : plan_kernel<Q.G, Q.CH, Q.NBUF, O | kSplitOpt>();
+            return prio ? plan_kernel<Q.G, Q.CH, Q.NBUF, Q.opt | SO>() : plan_kernel<Q.G, Q.CH, Q.NBUF, O | SO>();
     }
     return prio ? plan_kernel<Q.G, Q.CH, Q.NBUF, Q.opt>() : plan_kernel<Q.G, Q.CH, Q.NBUF, O>();
 }
