@@ -207,8 +207,9 @@ int priskv_crc32_blocks_plan(const priskv_crc_ctx *ctx, const void *d_base, uint
  * nblocks x block_size bytes at d_base with exactly the loads, per-wave
  * ranges, pipeline depth and XCD split crc_rows_kernel uses for this block
  * size (block_size a multiple of 4 KiB, d_base 16-byte aligned), without
- * hashing, and stores one word per wave into d_sink (nblocks uint32 entries;
- * which entries are written is unspecified).  Timing it beside
+ * hashing; each wave XORs the XOR of the 32-bit words it read into one entry
+ * of d_sink (nblocks uint32 entries; which entries is unspecified), so with
+ * a zeroed sink the XOR of all its entries is the XOR of the batch's words.  Timing it beside
  * priskv_crc32_blocks_dev on the same region gives the fraction of what HBM
  * delivers for this pattern that the CRC reaches.  Asynchronous on stream;
  * 0 or -EINVAL / -ENODEV / -EIO. */

@@ -408,6 +408,32 @@ def test_few_large_extents(torch_cuda, ctx, ctx_noseg, lens):
     assert np.array_equal(got, want)
 
 
+def test_read_roof_dev(torch_cuda, ctx):
+    """priskv_crc_read_roof_dev (diagnostic read roof of the CRC kernel's
+    access pattern): runs for the plans bench.py measures (4 KiB, 64 KiB,
+    1 MiB incl. the split mode, few large blocks), XORs each wave's XOR of
+    its words into the zeroed sink -- the XOR of the sink equals the XOR of
+    the whole region's 32-bit words -- and refuses what it cannot mirror
+    (block sizes not multiples of 4 KiB, unaligned bases)."""
+    import errno
+    torch = torch_cuda
+    t = _region(torch, ctx, 256 << 20, SEED ^ 0x2F, 17)
+    words = t[:256 << 20].view(torch.int32)
+    want = int(np.bitwise_xor.reduce(words.cpu().numpy().view(np.uint32)))
+    for bs in (4096, 65536, 1 << 20, 64 << 20, 256 << 20):
+        nb = (256 << 20) // bs
+        sink = torch.zeros(nb, dtype=torch.int32, device="cuda")
+        ctx.read_roof_dev(t, bs, sink, nblocks=nb)
+        torch.cuda.synchronize()
+        got = int(np.bitwise_xor.reduce(sink.cpu().numpy().view(np.uint32)))
+        assert got == want, (bs, hex(got), hex(want))
+    sink = torch.zeros(16, dtype=torch.int32, device="cuda")
+    for bs, off in ((1024, 0), (4100, 0), (4096, 4)):
+        with pytest.raises(OSError) as e:
+            ctx.read_roof_dev(t[off:], bs, sink, nblocks=4)
+        assert e.value.errno == errno.EINVAL
+
+
 def test_verify_dev(torch_cuda, ctx):
     """Device verify: CRC each value where it landed and compare with the
     expected CRCs (the oracle's); corrupted values are counted and the first
