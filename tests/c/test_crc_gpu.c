@@ -5,7 +5,10 @@
  * (server/test/test_kv.c): standalone executable, "[OK]"/"[FAILED]" lines,
  * non-zero exit on failure.  Every GPU result is checked against the host
  * priskv_crc32 from the same library, which test_crc_host.c and the pytest
- * suite pin to the reference server/crc.c.
+ * suite pin to the reference server/crc.c, and every block and value result
+ * also against the test-only oracle (oracle/liboracle_crc.so, the CPU
+ * restatement of server/crc.c:90-109, loaded with dlopen: a checker, not
+ * linked into anything the product ships).
  *
  *   blocks_dev    4 KiB / 64 KiB / 1 MiB / 4100-B / 256-B blocks, on a stream
  *   ranges_dev    PrisKV-shaped values (value_off on a 4 KiB block, valuelen ragged)
@@ -14,11 +17,15 @@
  *   blocks_host   the host-streamed block path
  *   errors        -EINVAL for bad arguments, -ENODEV for a missing device
  */
+#include <dlfcn.h>
 #include <errno.h>
+#include <libgen.h>
+#include <limits.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <unistd.h>
 
 #include <hip/hip_runtime_api.h>
 
@@ -51,8 +58,29 @@ static void report(const char *name, int before)
 
 #define REGION (64u << 20)
 
+/* the test-only oracle, next to this executable's tree: ../../oracle/ */
+static uint32_t (*oracle_crc32)(const void *, uint64_t);
+
+static void load_oracle(void)
+{
+    char exe[PATH_MAX], so[PATH_MAX + 64];
+    const ssize_t n = readlink("/proc/self/exe", exe, sizeof(exe) - 1);
+    if (n <= 0) {
+        printf("cannot resolve /proc/self/exe\n");
+        exit(2);
+    }
+    exe[n] = 0;
+    snprintf(so, sizeof(so), "%s/../../oracle/liboracle_crc.so", dirname(exe));
+    void *h = dlopen(so, RTLD_NOW | RTLD_LOCAL);
+    if (!h || !(*(void **)&oracle_crc32 = dlsym(h, "oracle_crc32"))) {
+        printf("oracle not loadable (%s): %s\n", so, dlerror());
+        exit(2);
+    }
+}
+
 int main(void)
 {
+    load_oracle();
     priskv_crc_ctx *ctx = NULL;
     int rc = priskv_crc_ctx_create(0, &ctx);
     if (rc) {
@@ -87,6 +115,11 @@ int main(void)
                     CHECK(0, "blocks_dev bs %u block %llu", bs, (unsigned long long)i);
                     break;
                 }
+            for (uint64_t i = 0; i < nb; i++) /* every block against the oracle */
+                if (h_out[i] != oracle_crc32(h_region + i * bs, bs)) {
+                    CHECK(0, "blocks_dev bs %u block %llu vs oracle", bs, (unsigned long long)i);
+                    break;
+                }
         }
         HIPOK(hipFree(d_out));
         free(h_out);
@@ -104,6 +137,7 @@ int main(void)
         offs[i] = ((x >> 40) % (REGION / 4096 - 4)) * 4096;
         lens[i] = span - (uint32_t)((x >> 20) % 4096);
         want[i] = priskv_crc32(h_region + offs[i], lens[i]);
+        CHECK(want[i] == oracle_crc32(h_region + offs[i], lens[i]), "host vs oracle, value %d", i);
     }
     uint64_t *d_offs;
     uint32_t *d_lens, *d_crc, *d_want;

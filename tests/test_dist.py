@@ -158,3 +158,52 @@ def test_gloo_world8_bench_collectives(fail_ranks):
         assert mx == 1.75
         assert ranks == list(range(world))
         assert alloc2
+
+
+def _gpu_worker(rank, world, port, bs, nblocks, q):
+    """One rank: its contiguous shard filled and hashed on the GPU (the
+    product path, priskv_crc32_blocks_dev), every rank's CRCs gathered."""
+    try:
+        import torch
+        import torch.distributed as dist
+        os.environ["MASTER_ADDR"] = "127.0.0.1"
+        os.environ["MASTER_PORT"] = str(port)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        from priskv_amd import CrcContext, as_u32
+        from priskv_amd.shard import gather_crcs
+        first, count = shard_blocks(nblocks, rank, world)
+        with CrcContext(0) as ctx:
+            region = torch.empty(bs * count, dtype=torch.uint8, device="cuda:0")
+            ctx.fill_splitmix(region, 0x5EED, shard_word_offset(first, bs))
+            local = as_u32(ctx.blocks_dev(region, bs))
+        allc = gather_crcs(local, nblocks)
+        dist.barrier()
+        q.put((rank, allc, None))
+        dist.destroy_process_group()
+    except BaseException as e:  # report instead of leaving the test to time out
+        q.put((rank, None, repr(e)))
+        raise
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("bs,nblocks", [(4096, 1 << 14), (1 << 20, 64)])
+def test_gloo_world2_gpu_shards(bs, nblocks):
+    """The N > 1 path with the GPU doing each rank's work: two ranks (one
+    GPU on the test box, so both on device 0) hash their shards through the
+    C ABI and gather; the result equals the oracle over the one global
+    region."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_gpu_worker, args=(r, world, port, bs, nblocks, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted((q.get(timeout=240) for _ in range(world)), key=lambda r: r[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    want = O.crc32_blocks(O.fill_splitmix(bs * nblocks, 0x5EED, 0), bs)
+    for rank, allc, err in res:
+        assert err is None, (rank, err)
+        assert np.array_equal(allc, want), rank
