@@ -1363,7 +1363,10 @@ int priskv_crc_read_roof_dev(const priskv_crc_ctx *ctx, const void *d_base, uint
         uint32_t bs = block_size;
         uint32_t xw = n >= 32ull * grid * kWaves ? ctx->plan_xw[p] : 0u;
         uint32_t ush = (uint32_t)log2u(S);
-        void *args[] = {(void *)&b, (void *)&n, (void *)&bs, (void *)&o, (void *)&xw, (void *)&ush};
+        uint32_t tile = S == 1 ? tile_groups(ctx, n, bs) : 0u; // the CRC kernel's tiles (G = 64: a group is a block)
+        if (tile)
+            xw = 0;
+        void *args[] = {(void *)&b, (void *)&n, (void *)&bs, (void *)&o, (void *)&xw, (void *)&ush, (void *)&tile};
         if (int rc = herr(hipLaunchKernel(fn, dim3(grid), dim3(kThreads), args, 0, (hipStream_t)stream)))
             return rc;
         done += n;

@@ -427,6 +427,17 @@ def test_read_roof_dev(torch_cuda, ctx):
         torch.cuda.synchronize()
         got = int(np.bitwise_xor.reduce(sink.cpu().numpy().view(np.uint32)))
         assert got == want, (bs, hex(got), hex(want))
+    tiles = _ctx_env(PRISKV_CRC_TILE_MIN_GIB="0")  # the block-cyclic tile order at any size
+    try:
+        for bs in (4096, 65536):
+            nb = (256 << 20) // bs
+            sink = torch.zeros(nb, dtype=torch.int32, device="cuda")
+            tiles.read_roof_dev(t, bs, sink, nblocks=nb)
+            torch.cuda.synchronize()
+            got = int(np.bitwise_xor.reduce(sink.cpu().numpy().view(np.uint32)))
+            assert got == want, ("tiles", bs, hex(got), hex(want))
+    finally:
+        tiles.close()
     sink = torch.zeros(16, dtype=torch.int32, device="cuda")
     for bs, off in ((1024, 0), (4100, 0), (4096, 4)):
         with pytest.raises(OSError) as e:
