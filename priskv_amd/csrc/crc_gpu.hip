@@ -70,6 +70,7 @@ struct priskv_crc_ctx {
     uint32_t plan_xw[16];      // rows-kernel split per plan: (even << 16) | odd XCD weight, 0 = equal
     int segment;               // split few large blocks / extents into segments (PRISKV_CRC_SEGMENT=0: off)
     int split;                 // rows kernel split mode for few blocks per wave (PRISKV_CRC_SPLIT=0: off)
+    int tune4k;                // TMP A/B: 4 KiB plan pipeline depth (PRISKV_CRC_TUNE4K)
     int prio;                  // rows kernel progress priority (PRISKV_CRC_PRIO=0: off)
     int balance;               // byte-balanced extents split (PRISKV_CRC_BALANCE=0: off)
     int head_split;            // rows kernel + head terms for B = h + whole KiB rows (PRISKV_CRC_HEADSPLIT=0: off)
@@ -553,7 +554,12 @@ int launch_plan(const priskv_crc_ctx *ctx, int p, const uint8_t *base, uint64_t 
         void *args[] = {(void *)&b,  (void *)&n,    (void *)&bs,   (void *)&img,    (void *)&fold,
                         (void *)&o,  (void *)&xw,   (void *)&tile, (void *)&stride, (void *)&one,
                         (void *)&zp, (void *)&none, (void *)&none};
-        if (int rc = herr(hipLaunchKernel(plan_fn(p, ctx->prio), dim3(grid), dim3(kThreads), args, 0, s)))
+        const void *fn = plan_fn(p, ctx->prio);
+        if (p == PLAN_4K && ctx->prio && ctx->tune4k == 4) // TMP A/B
+            fn = plan_kernel<64, 4, 4, kPlans[PLAN_4K].opt>();
+        else if (p == PLAN_4K && ctx->prio && ctx->tune4k == 5)
+            fn = plan_kernel<64, 4, 5, kPlans[PLAN_4K].opt>();
+        if (int rc = herr(hipLaunchKernel(fn, dim3(grid), dim3(kThreads), args, 0, s)))
             return rc;
         done += n;
     }
@@ -1405,6 +1411,7 @@ int priskv_crc_ctx_create(int device, priskv_crc_ctx **out)
     {
         const char *e = getenv("PRISKV_CRC_SEGMENT");
         c->segment = !(e && !strcmp(e, "0"));
+        c->tune4k = getenv("PRISKV_CRC_TUNE4K") ? atoi(getenv("PRISKV_CRC_TUNE4K")) : 3;
         const char *sp = getenv("PRISKV_CRC_SPLIT");
         c->split = !(sp && !strcmp(sp, "0"));
         const char *pe = getenv("PRISKV_CRC_PRIO");
