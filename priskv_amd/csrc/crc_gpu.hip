@@ -70,7 +70,6 @@ struct priskv_crc_ctx {
     uint32_t plan_xw[16];      // rows-kernel split per plan: (even << 16) | odd XCD weight, 0 = equal
     int segment;               // split few large blocks / extents into segments (PRISKV_CRC_SEGMENT=0: off)
     int split;                 // rows kernel split mode for few blocks per wave (PRISKV_CRC_SPLIT=0: off)
-    int tune4k;                // TMP A/B: 4 KiB plan pipeline depth (PRISKV_CRC_TUNE4K)
     int prio;                  // rows kernel progress priority (PRISKV_CRC_PRIO=0: off)
     int balance;               // byte-balanced extents split (PRISKV_CRC_BALANCE=0: off)
     int head_split;            // rows kernel + head terms for B = h + whole KiB rows (PRISKV_CRC_HEADSPLIT=0: off)
@@ -400,6 +399,7 @@ enum PlanId {
     PLAN_G64_CH2,
     PLAN_G64_CH1,
     PLAN_SPLIT_DEEP,   // split mode for few large blocks: G64, CH4, 3 chunks in flight, first chunks before the tables
+    PLAN_4K_DEEP,      // 4 KiB in batches of >= 1 GiB: the 4 KiB plan with 4 chunks in flight
     NPLANS
 };
 static_assert(NPLANS <= 16, "priskv_crc_ctx per-plan arrays");
@@ -428,12 +428,20 @@ constexpr Plan kPlans[NPLANS] = {
     {64, 4, 3, 2 | kEarly | 32 | kPrio3, 1, 31, 29}, {64, 4, 2, 32 | kPrio1, 1, 31, 29}, {16, 4, 2, 2 | 32 | kPrio1, 1, 31, 29},
     {16, 4, 2, kPrio1, 1, 31, 29},          {64, 4, 2, kPrio1, 1, 31, 29},      {64, 4, 2, kPrio3, 1, 31, 29},
     {64, 2, 2, 0, 1, 31, 29},               {64, 1, 2, 0, 1, 31, 29},
-    {64, 4, 3, kEarly | 32 | kPrio3, 1, 31, 29}};
+    {64, 4, 3, kEarly | 32 | kPrio3, 1, 31, 29},
+    {64, 4, 4, 2 | kEarly | 32 | kPrio3, 1, 31, 29}};
 
-int plan_for(uint32_t bs)
+// 4 KiB blocks in batches of at least this many: four chunks in flight
+// instead of three, +0.4-0.5 % at 4 GiB on every one of 6 allocations on two
+// boxes (same process, profiles/r04/nbuf4k/), while 256 MiB calls are level
+// to 2 % slower (a longer pipeline fill); round 2 measured 4 deep -0.9 % at
+// 4 GiB on round 2's code
+constexpr uint64_t kDeep4kBlocks = 1ull << 18; // 1 GiB
+
+int plan_for(uint32_t bs, uint64_t nblocks = 0)
 {
     if (bs == 4096)
-        return PLAN_4K;
+        return nblocks >= kDeep4kBlocks ? PLAN_4K_DEEP : PLAN_4K;
     if (bs == 8192)
         return PLAN_G64_CH4_NIB;
     if (bs == 1024)
@@ -487,6 +495,7 @@ const void *plan_fn(int p, bool prio, bool split = false)
     case PLAN_G64_CH4_BIG: return plan_kernel_p<PLAN_G64_CH4_BIG>(prio, split);
     case PLAN_G64_CH2: return plan_kernel_p<PLAN_G64_CH2>(prio, split);
     case PLAN_SPLIT_DEEP: return plan_kernel_p<PLAN_SPLIT_DEEP>(prio, split);
+    case PLAN_4K_DEEP: return plan_kernel_p<PLAN_4K_DEEP>(prio, split);
     default: return plan_kernel_p<PLAN_G64_CH1>(prio, split);
     }
 }
@@ -554,12 +563,7 @@ int launch_plan(const priskv_crc_ctx *ctx, int p, const uint8_t *base, uint64_t 
         void *args[] = {(void *)&b,  (void *)&n,    (void *)&bs,   (void *)&img,    (void *)&fold,
                         (void *)&o,  (void *)&xw,   (void *)&tile, (void *)&stride, (void *)&one,
                         (void *)&zp, (void *)&none, (void *)&none};
-        const void *fn = plan_fn(p, ctx->prio);
-        if (p == PLAN_4K && ctx->prio && ctx->tune4k == 4) // TMP A/B
-            fn = plan_kernel<64, 4, 4, kPlans[PLAN_4K].opt>();
-        else if (p == PLAN_4K && ctx->prio && ctx->tune4k == 5)
-            fn = plan_kernel<64, 4, 5, kPlans[PLAN_4K].opt>();
-        if (int rc = herr(hipLaunchKernel(fn, dim3(grid), dim3(kThreads), args, 0, s)))
+        if (int rc = herr(hipLaunchKernel(plan_fn(p, ctx->prio), dim3(grid), dim3(kThreads), args, 0, s)))
             return rc;
         done += n;
     }
@@ -834,7 +838,7 @@ int launch_rows_plain(const priskv_crc_ctx *ctx, const uint8_t *base, uint64_t n
 {
     if (!stride)
         stride = bs;
-    const int p = plan_for(bs);
+    const int p = plan_for(bs, nblocks);
     const uint64_t per = 64 / kPlans[p].G; // blocks per wave group
     const uint64_t head = nblocks - nblocks % per;
     if (head)
@@ -1294,7 +1298,7 @@ int priskv_crc32_blocks_plan(const priskv_crc_ctx *ctx, const void *d_base, uint
         block_size -= hb;
         const uint32_t S = segments_for(ctx, nblocks, block_size);
         const uint32_t bs = block_size / S;
-        const int p = plan_for(bs);
+        const int p = plan_for(bs, nblocks * S);
         const Plan &P = kPlans[p];
         const uint32_t xw = ctx->plan_xw[p];
         const int mode = ctx->prio ? (P.opt >> 8) & 3 : 0;
@@ -1345,7 +1349,7 @@ int priskv_crc_read_roof_dev(const priskv_crc_ctx *ctx, const void *d_base, uint
     // its resident workgroups, its split mode (units of block_size / S) and
     // its XCD weights (only with many units per wave, as launch_plan applies
     // them); the roof reads units as blocks
-    int p = plan_for(block_size);
+    int p = plan_for(block_size, nblocks);
     uint32_t S = 1;
     if (segments_for(ctx, nblocks, block_size) == 1)
         S = split_for(ctx, nblocks, block_size);
@@ -1358,8 +1362,9 @@ int priskv_crc_read_roof_dev(const priskv_crc_ctx *ctx, const void *d_base, uint
     const uint64_t cps = block_size / 4096;
     const uint64_t cap = max_wgs * kWaves * ((1ull << 31) / cps - 1);
     const uint8_t *base = static_cast<const uint8_t *>(d_base);
-    const void *fn = P.NBUF == 3 ? reinterpret_cast<const void *>(&crc_read_roof_kernel<4, 3, kAux>)
-                                 : reinterpret_cast<const void *>(&crc_read_roof_kernel<4, 2, kAux>);
+    const void *fn = P.NBUF == 4   ? reinterpret_cast<const void *>(&crc_read_roof_kernel<4, 4, kAux>)
+                     : P.NBUF == 3 ? reinterpret_cast<const void *>(&crc_read_roof_kernel<4, 3, kAux>)
+                                   : reinterpret_cast<const void *>(&crc_read_roof_kernel<4, 2, kAux>);
     for (uint64_t done = 0; done < nblocks;) {
         uint64_t n = nblocks - done < cap ? nblocks - done : cap;
         const uint64_t want = (n + kWaves - 1) / kWaves;
@@ -1411,7 +1416,6 @@ int priskv_crc_ctx_create(int device, priskv_crc_ctx **out)
     {
         const char *e = getenv("PRISKV_CRC_SEGMENT");
         c->segment = !(e && !strcmp(e, "0"));
-        c->tune4k = getenv("PRISKV_CRC_TUNE4K") ? atoi(getenv("PRISKV_CRC_TUNE4K")) : 3;
         const char *sp = getenv("PRISKV_CRC_SPLIT");
         c->split = !(sp && !strcmp(sp, "0"));
         const char *pe = getenv("PRISKV_CRC_PRIO");

@@ -1188,7 +1188,10 @@ def test_xcd_weights_probe_fallback_and_tiles(torch_cuda, ctx, bs):
 def test_blocks_plan_strings(torch_cuda, ctx):
     """priskv_crc32_blocks_plan names the kernel blocks_dev launches."""
     base = 1 << 20  # any 16-B aligned address: the plan does not dereference it
-    assert ctx.blocks_plan(base, 1 << 20, 4096).startswith("crc_rows_kernel<G=64,CH=4,NBUF=3,nt,pipelined-fold,"
+    # 4 KiB: 4 chunks in flight from 1 GiB per call, 3 below
+    assert ctx.blocks_plan(base, 1 << 20, 4096).startswith("crc_rows_kernel<G=64,CH=4,NBUF=4,nt,pipelined-fold,"
+                                                             "nibble-fold,progress-priority 3")
+    assert ctx.blocks_plan(base, 1 << 16, 4096).startswith("crc_rows_kernel<G=64,CH=4,NBUF=3,nt,pipelined-fold,"
                                                              "nibble-fold,progress-priority 3")
     assert ctx.blocks_plan(base, 1 << 16, 65536).startswith("crc_rows_kernel<G=64,CH=4,NBUF=2,nt,progress-priority 1")
     # the 128 GiB shard of BASELINE configs[3] runs in block-cyclic 1 MiB tiles
