@@ -70,7 +70,6 @@ struct priskv_crc_ctx {
     uint32_t plan_xw[16];      // rows-kernel split per plan: (even << 16) | odd XCD weight, 0 = equal
     int segment;               // split few large blocks / extents into segments (PRISKV_CRC_SEGMENT=0: off)
     int split;                 // rows kernel split mode for few blocks per wave (PRISKV_CRC_SPLIT=0: off)
-    int tune_nb;               // TMP A/B
     int prio;                  // rows kernel progress priority (PRISKV_CRC_PRIO=0: off)
     int balance;               // byte-balanced extents split (PRISKV_CRC_BALANCE=0: off)
     int head_split;            // rows kernel + head terms for B = h + whole KiB rows (PRISKV_CRC_HEADSPLIT=0: off)
@@ -546,10 +545,7 @@ int launch_plan(const priskv_crc_ctx *ctx, int p, const uint8_t *base, uint64_t 
         void *args[] = {(void *)&base, (void *)&n,    (void *)&bs,    (void *)&img,   (void *)&fold,
                         (void *)&out,  (void *)&xw,   (void *)&tile,  (void *)&stride, (void *)&split,
                         (void *)&zp,   (void *)&cnt,  (void *)&xacc};
-        const void *fn = plan_fn(p, ctx->prio, true);
-        if (ctx->tune_nb == 3 && ctx->prio && p == PLAN_G64_CH4_BIG) // TMP A/B
-            fn = plan_kernel<64, 4, 3, kPlans[PLAN_G64_CH4_BIG].opt | kSplitOpt>();
-        return herr(hipLaunchKernel(fn, dim3(grid), dim3(kThreads), args, 0, s));
+        return herr(hipLaunchKernel(plan_fn(p, ctx->prio, true), dim3(grid), dim3(kThreads), args, 0, s));
     }
     // the kernel counts a wave's chunks in 32 bits: cap groups per launch
     const uint64_t cap = max_wgs * kWaves * ((1ull << 31) / cps - 1);
@@ -567,12 +563,7 @@ int launch_plan(const priskv_crc_ctx *ctx, int p, const uint8_t *base, uint64_t 
         void *args[] = {(void *)&b,  (void *)&n,    (void *)&bs,   (void *)&img,    (void *)&fold,
                         (void *)&o,  (void *)&xw,   (void *)&tile, (void *)&stride, (void *)&one,
                         (void *)&zp, (void *)&none, (void *)&none};
-        const void *fn = plan_fn(p, ctx->prio);
-        if (ctx->tune_nb == 3 && ctx->prio && p == PLAN_G64_CH4) // TMP A/B
-            fn = plan_kernel<64, 4, 3, kPlans[PLAN_G64_CH4].opt>();
-        else if (ctx->tune_nb == 3 && ctx->prio && p == PLAN_G64_CH4_BIG)
-            fn = plan_kernel<64, 4, 3, kPlans[PLAN_G64_CH4_BIG].opt>();
-        if (int rc = herr(hipLaunchKernel(fn, dim3(grid), dim3(kThreads), args, 0, s)))
+        if (int rc = herr(hipLaunchKernel(plan_fn(p, ctx->prio), dim3(grid), dim3(kThreads), args, 0, s)))
             return rc;
         done += n;
     }
@@ -1425,7 +1416,6 @@ int priskv_crc_ctx_create(int device, priskv_crc_ctx **out)
     {
         const char *e = getenv("PRISKV_CRC_SEGMENT");
         c->segment = !(e && !strcmp(e, "0"));
-        c->tune_nb = getenv("PRISKV_CRC_TUNE_NB") ? atoi(getenv("PRISKV_CRC_TUNE_NB")) : 0;
         const char *sp = getenv("PRISKV_CRC_SPLIT");
         c->split = !(sp && !strcmp(sp, "0"));
         const char *pe = getenv("PRISKV_CRC_PRIO");
