@@ -1035,6 +1035,39 @@ _SPLIT_CASES = [(1 << 20, 1900), (1 << 20, 4096), (512 << 10, 4000), (256 << 10,
                 (12 << 20, 3)]
 
 
+def test_rows_split_mode_graph_capture(torch_cuda, ctx):
+    """Split mode under HIP graph capture: its zero-at-rest counters come from
+    stream-ordered scratch (allocated and zeroed inside the graph), and every
+    replay on new data is exact -- a balanced 1 MiB batch and one 256 MiB block
+    (the few-large-blocks plan), captured into one graph."""
+    torch = torch_cuda
+    n = 1900 << 20
+    t = _region(torch, ctx, n, SEED ^ 0x5B1, 3)
+    big = t[: 256 << 20]
+    o1 = torch.empty(1900, dtype=torch.int32, device="cuda")
+    o2 = torch.empty(1, dtype=torch.int32, device="cuda")
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        ctx.blocks_dev(t, 1 << 20, out=o1, nblocks=1900, stream=s)
+        ctx.blocks_dev(big, 256 << 20, out=o2, nblocks=1, stream=s)
+    torch.cuda.current_stream().wait_stream(s)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        st = torch.cuda.current_stream()
+        ctx.blocks_dev(t, 1 << 20, out=o1, nblocks=1900, stream=st)
+        ctx.blocks_dev(big, 256 << 20, out=o2, nblocks=1, stream=st)
+    for seed in (21, 22):
+        ctx.fill_splitmix(t, seed, 0)
+        g.replay()
+        g.replay()  # back to back: the counters are left zero by each launch
+        torch.cuda.synchronize()
+        host = t[:n].cpu().numpy()
+        assert np.array_equal(_u32(o1), O.crc32_blocks(host, 1 << 20, nthreads=16))
+        assert np.array_equal(_u32(o2), O.crc32_blocks(host[: 256 << 20], 256 << 20, nthreads=16))
+
+
 @pytest.mark.parametrize("bs,nb", _SPLIT_CASES)
 def test_rows_split_mode(torch_cuda, ctx, bs, nb):
     """crc_rows_kernel's split mode (OPT bit 6): few blocks per wave cut into
