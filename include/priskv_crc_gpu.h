@@ -73,8 +73,9 @@ int priskv_crc32_blocks_dev(const priskv_crc_ctx *ctx, const void *d_base, uint6
  * d_out are device arrays of n entries.  Asynchronous on `stream`.  With few
  * extents (n <= 8192; PRISKV_CRC_SEG_MAX_EXTENTS) each is split into segments
  * on the device; with a few extents per resident wave the split over the
- * waves is balanced by bytes.  Both need a small scratch allocation ordered
- * on `stream` (hipMallocAsync); -ENOMEM if that fails. */
+ * waves is balanced by bytes.  Both need a small scratch allocation: a
+ * context pool slot owned by `stream` (the first stream to take a slot keeps
+ * it), else one ordered on `stream` (hipMallocAsync); -ENOMEM if that fails. */
 int priskv_crc32_ranges_dev(const priskv_crc_ctx *ctx, const void *d_base,
                             const uint64_t *d_offsets, const uint32_t *d_lengths, uint64_t n,
                             uint32_t *d_out, void *stream);

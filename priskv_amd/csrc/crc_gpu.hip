@@ -57,9 +57,9 @@ namespace {
 struct priskv_crc_pool_slot {
     void *p;
     size_t size;
-    hipEvent_t ev; // recorded after the slot's last use
-    int busy;      // taken by a call in flight on the host
-    int used;      // ev has been recorded at least once
+    hipStream_t home; // the one stream that uses the slot
+    int homed;               // home is set (the slot has been taken once)
+    int busy;                // taken by a call in flight on the host
 };
 
 struct priskv_crc_ctx {
@@ -148,12 +148,19 @@ inline int herr(hipError_t e)
 }
 
 // Scratch for one *_dev call.  Outside stream capture it comes from the
-// context's pool: the slot's previous use is ordered before this one by a
-// wait on the event its release recorded (so any stream may take any free
-// slot), which saves the stream-ordered alloc/free pair, ~6 us of host time
-// per call against ~1 us for the event pair (profiles/r01/host_cost_r4k.json).
-// While the stream is capturing, or with every slot taken, it is a per-call
-// hipMallocAsync / hipFreeAsync as before, so a captured graph owns its own.
+// context's pool, which saves the stream-ordered alloc/free pair (~6 us of
+// host time per call, profiles/r01/host_cost_r4k.json).  A slot belongs to
+// the first stream that takes it and only that stream takes it again, so
+// stream order alone puts its previous use first -- no event.  (A handle
+// stays taken while its stream has work: a destroyed stream's object lives
+// until that work completes, so a new stream cannot alias it meanwhile.)  Rounds 1-3 recorded an event per release so that any stream could
+// take any slot: that marker packet idled the queue ~5 us before the next
+// call's kernel (1 x 256 MiB 54.7 -> 49.9 us per call without it; also with
+// the event carried by the kernel launch itself, hipExtLaunchKernel, 4.6 us:
+// profiles/r04/pool_event/).  With no free slot of the stream's own or
+// unowned (more concurrent streams than slots), while the stream is
+// capturing, or with the pool off, it is a per-call hipMallocAsync /
+// hipFreeAsync, so a captured graph owns its own.
 //
 // zero: the memory must read as zeros when a call gets it.  Then `slots` is a
 // pool whose users leave their slot zeroed (the fused extents kernel's
@@ -180,12 +187,14 @@ struct Scratch {
     int get(size_t bytes)
     {
         hipStreamCaptureStatus cs = hipStreamCaptureStatusActive;
+        const hipStream_t sid = s;
         if (ctx->pool_ready && hipStreamIsCapturing(s, &cs) == hipSuccess && cs == hipStreamCaptureStatusNone) {
             pthread_mutex_lock(&ctx->pool_lock);
-            int fit = -1, grow = -1; // smallest free slot that fits, else the largest free one
+            // smallest free slot of this stream (or unowned) that fits, else the largest
+            int fit = -1, grow = -1;
             for (int i = 0; i < NPOOL; i++) {
                 const priskv_crc_pool_slot &q = slots[i];
-                if (q.busy)
+                if (q.busy || (q.homed && q.home != sid))
                     continue;
                 if (q.size >= bytes) {
                     if (fit < 0 || q.size < slots[fit].size)
@@ -195,18 +204,21 @@ struct Scratch {
                 }
             }
             const int k = fit >= 0 ? fit : grow;
-            if (k >= 0)
+            if (k >= 0) {
                 slots[k].busy = 1;
+                slots[k].homed = 1;
+                slots[k].home = sid;
+            }
             pthread_mutex_unlock(&ctx->pool_lock);
             if (k >= 0) {
                 priskv_crc_pool_slot &q = slots[k];
-                int rc = q.used ? herr(hipStreamWaitEvent(s, q.ev, 0)) : 0;
-                if (!rc && q.size < bytes) {
+                int rc = 0;
+                if (q.size < bytes) {
                     size_t cap = 64u << 10;
                     while (cap < bytes)
                         cap *= 2;
                     if (q.p)
-                        rc = herr(hipFreeAsync(q.p, s)); // ordered after the wait
+                        rc = herr(hipFreeAsync(q.p, s)); // after the slot's last use: same stream
                     q.p = nullptr;
                     q.size = 0;
                     if (!rc && !(rc = herr(hipMallocAsync(&q.p, cap, s))))
@@ -236,17 +248,12 @@ struct Scratch {
         if (slot < 0)
             return p ? herr(hipFreeAsync(p, s)) : 0;
         priskv_crc_pool_slot &q = slots[slot];
-        int rc = herr(hipEventRecord(q.ev, s));
-        if (rc)
-            (void)hipStreamSynchronize(s); // the slot is idle before anyone reuses it
-        else
-            q.used = 1;
         pthread_mutex_lock(&ctx->pool_lock);
         q.busy = 0;
         pthread_mutex_unlock(&ctx->pool_lock);
         slot = -1;
         p = nullptr;
-        return rc;
+        return 0;
     }
 };
 
@@ -1511,12 +1518,8 @@ int priskv_crc_ctx_create(int device, priskv_crc_ctx **out)
     for (int p = 0; p < NPLANS; p++)
         c->plan_xw[p] = xcd_weights(c->xcd_rr, p);
     {
-        int ev_ok = 1; // without the events every call keeps its own alloc/free
-        for (int i = 0; i < NPOOL; i++)
-            ev_ok = ev_ok && hipEventCreateWithFlags(&c->pool[i].ev, hipEventDisableTiming) == hipSuccess &&
-                    hipEventCreateWithFlags(&c->cnt_pool[i].ev, hipEventDisableTiming) == hipSuccess;
         const char *pe = getenv("PRISKV_CRC_SCRATCH_POOL");
-        c->pool_ready = ev_ok && !(pe && !strcmp(pe, "0"));
+        c->pool_ready = !(pe && !strcmp(pe, "0"));
     }
     free(h_img);
     free(h_fold);
@@ -1556,16 +1559,20 @@ void priskv_crc_ctx_destroy(priskv_crc_ctx *c)
     (void)hipFree(c->d_rowshift);
     (void)hipFree(c->d_zpow);
     (void)hipFree(c->d_scrub);
-    for (priskv_crc_pool_slot *slots : {c->pool, c->cnt_pool})
-        for (int i = 0; i < NPOOL; i++) {
-            priskv_crc_pool_slot &q = slots[i];
-            if (q.used)
-                (void)hipEventSynchronize(q.ev);
-            if (q.p)
-                (void)hipFreeAsync(q.p, c->aux);
-            if (q.ev)
-                (void)hipEventDestroy(q.ev);
-        }
+    {
+        // the slots' last uses are on their home streams, which may be gone
+        // by now: wait for the device before freeing them
+        bool any = false;
+        for (priskv_crc_pool_slot *slots : {c->pool, c->cnt_pool})
+            for (int i = 0; i < NPOOL; i++)
+                any = any || slots[i].p;
+        if (any)
+            (void)hipDeviceSynchronize();
+        for (priskv_crc_pool_slot *slots : {c->pool, c->cnt_pool})
+            for (int i = 0; i < NPOOL; i++)
+                if (slots[i].p)
+                    (void)hipFreeAsync(slots[i].p, c->aux);
+    }
     if (c->aux) {
         (void)hipStreamSynchronize(c->aux);
         (void)hipStreamDestroy(c->aux);
