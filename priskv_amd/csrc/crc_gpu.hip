@@ -1635,9 +1635,8 @@ int priskv_crc32_verify_dev(const priskv_crc_ctx *ctx, const void *d_base, const
         return -ENODEV;
     hipStream_t s = (hipStream_t)stream;
     // status first: a zero-length verify still reports {0, UINT64_MAX}
-    if (int rc = herr(hipMemsetAsync(d_status, 0, sizeof(uint64_t), s)))
-        return rc;
-    if (int rc = herr(hipMemsetAsync(d_status + 1, 0xFF, sizeof(uint64_t), s)))
+    hipLaunchKernelGGL(crc_status_init_kernel, dim3(1), dim3(64), 0, s, (unsigned long long *)d_status);
+    if (int rc = herr(hipGetLastError()))
         return rc;
     if (n == 0)
         return 0;

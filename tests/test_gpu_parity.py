@@ -1036,6 +1036,43 @@ _SPLIT_CASES = [(1 << 20, 1900), (1 << 20, 4096), (512 << 10, 4000), (256 << 10,
                 (12 << 20, 3)]
 
 
+def test_verify_graph_capture(torch_cuda, ctx):
+    """verify_dev captured into a HIP graph: its status words are set by a
+    write-through init kernel and then only updated by atomics, so replays
+    back to back report exactly the mismatches of the current data."""
+    torch = torch_cuda
+    n = 64 << 20
+    t = _region(torch, ctx, n, SEED ^ 0x7E, 1)
+    rng = np.random.default_rng(77)
+    cnt = 5000  # many values: the plain extents path
+    lens = rng.integers(1, 16 << 10, cnt).astype(np.uint32)
+    offs = np.array([rng.integers(0, n - int(ln)) for ln in lens], dtype=np.uint64)
+    d_o = torch.from_numpy(offs.astype(np.int64)).cuda()
+    d_l = torch.from_numpy(lens.view(np.int32)).cuda()
+    want = O.crc32_ranges(t[:n].cpu().numpy(), offs, lens)
+    exp = torch.from_numpy(want.view(np.int32)).cuda()
+    status = torch.empty(2, dtype=torch.int64, device="cuda")
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        ctx.verify_dev(t, d_o, d_l, exp, status=status, stream=s)
+    torch.cuda.current_stream().wait_stream(s)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        ctx.verify_dev(t, d_o, d_l, exp, status=status, stream=torch.cuda.current_stream())
+    for bad in ([], [4321], [17, 4000, 4999]):
+        e = want.copy()
+        for i in bad:
+            e[i] ^= 1
+        exp.copy_(torch.from_numpy(e.view(np.int32)))
+        g.replay()
+        g.replay()
+        torch.cuda.synchronize()
+        st = status.tolist()
+        assert st[0] == len(bad) and st[1] == (min(bad) if bad else -1), (bad, st)
+
+
 def test_rows_split_mode_graph_capture(torch_cuda, ctx):
     """Split mode under HIP graph capture: its zero-at-rest counters come from
     stream-ordered scratch (allocated and zeroed inside the graph), and every
