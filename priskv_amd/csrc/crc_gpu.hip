@@ -435,7 +435,7 @@ constexpr Plan kPlans[NPLANS] = {
     {64, 4, 3, 2 | kEarly | 32 | kPrio3, 1, 31, 29}, {64, 4, 2, 32 | kPrio1, 1, 31, 29}, {16, 4, 2, 2 | 32 | kPrio1, 1, 31, 29},
     {16, 4, 2, kPrio1, 1, 31, 29},          {64, 4, 2, kPrio1, 1, 31, 29},      {64, 4, 2, kPrio3, 1, 31, 29},
     {64, 2, 2, 0, 1, 31, 29},               {64, 1, 2, 0, 1, 31, 29},
-    {64, 4, 3, kEarly | 32 | kPrio3, 1, 31, 29},
+    {64, 4, 3, kEarly | 32 | kPrio3, 1, 31, 29}, // (4 deep: 1 x 256 MiB +1.8 %, 16 x 16 MiB +3.2 % slower, profiles/r04/split/split_deep_nbuf4_ab.jsonl)
     {64, 4, 4, 2 | kEarly | 32 | kPrio3, 1, 31, 29}};
 
 // 4 KiB blocks in batches of at least this many: four chunks in flight
@@ -620,7 +620,9 @@ constexpr uint32_t kSplitMinUnit = 16u << 10;
 uint32_t split_for(const priskv_crc_ctx *ctx, uint64_t nblocks, uint32_t bs)
 {
     const int p = plan_for(bs);
-    if (!ctx->split || !plan_splits(p) || !ctx->plan_xw[p] || bs % 4096 != 0)
+    // (block-cyclic tiles win where both apply: batches of >= 64 GiB, or
+    // PRISKV_CRC_TILE_MIN_GIB; split plans are G = 64, one block per group)
+    if (!ctx->split || !plan_splits(p) || !ctx->plan_xw[p] || bs % 4096 != 0 || tile_groups(ctx, nblocks, bs))
         return 1;
     const uint64_t want = kSplitUnitsPerWave * (uint64_t)ctx->num_cus * ctx->plan_wgs_per_cu[p] * kWaves;
     if (nblocks >= want)
