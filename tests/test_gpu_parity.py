@@ -915,6 +915,55 @@ def test_concurrent_streams_and_threads(torch_cuda, ctx):
             assert np.array_equal(a, want[k][0]) and np.array_equal(b, want[k][1]) and np.array_equal(c, want[k][2])
 
 
+def test_threads_sharing_one_stream(torch_cuda, ctx):
+    """4 host threads enqueue scratch-needing calls (segmented extents, split
+    few large blocks, fused) on ONE shared stream with no host sync between
+    them: pooled slots are owned per stream, so the calls in flight hold
+    different slots of that stream (or allocate per call) and stream order
+    keeps each slot's uses apart.  Every result must equal the oracle's."""
+    import threading
+    torch = torch_cuda
+    region = _region(torch, ctx, 96 << 20, SEED ^ 0xD1, 1)
+    torch.cuda.synchronize()
+    host = region[: 96 << 20].cpu().numpy()
+    rng = np.random.default_rng(31)
+    shared = torch.cuda.Stream()
+    shared.wait_stream(torch.cuda.current_stream())
+    jobs = []
+    for k in range(4):
+        lens = rng.integers(1 << 20, 8 << 20, 3 + k).astype(np.uint32)
+        offs = np.array([rng.integers(0, (96 << 20) - int(ln)) for ln in lens], dtype=np.uint64)
+        jobs.append((offs, lens, torch.from_numpy(offs.astype(np.int64)).cuda(),
+                     torch.from_numpy(lens.view(np.int32)).cuda()))
+    torch.cuda.synchronize()
+    want = [O.crc32_ranges(host, o, ln) for o, ln, _, _ in jobs]
+    want_b = O.crc32_blocks(host[: 32 << 20], 16 << 20, nthreads=4)
+    got, errs = [None] * len(jobs), []
+
+    def run(k):
+        try:
+            _, _, d_o, d_l = jobs[k]
+            res = []
+            for _ in range(6):
+                with torch.cuda.stream(shared):
+                    res.append((ctx.ranges_dev(region, d_o, d_l, stream=shared),
+                                ctx.blocks_dev(region, 16 << 20, nblocks=2, stream=shared)))
+            got[k] = res
+        except Exception as e:  # surfaced below
+            errs.append(e)
+
+    th = [threading.Thread(target=run, args=(k,)) for k in range(len(jobs))]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    shared.synchronize()
+    assert not errs, errs
+    for k in range(len(jobs)):
+        for a, b in got[k]:
+            assert np.array_equal(_u32(a), want[k]) and np.array_equal(_u32(b), want_b), k
+
+
 def test_hip_graph_capture_and_replay(torch_cuda, ctx):
     """The *_dev calls are pure stream work (kernels, stream-ordered scratch):
     they capture into a HIP graph and replay on new data with correct results --
