@@ -153,8 +153,9 @@ inline int herr(hipError_t e)
 // the first stream that takes it and only that stream takes it again, so
 // stream order alone puts its previous use first -- no event.  (A handle
 // stays taken while its stream has work: a destroyed stream's object lives
-// until that work completes, so a new stream cannot alias it meanwhile.)  Rounds 1-3 recorded an event per release so that any stream could
-// take any slot: that marker packet idled the queue ~5 us before the next
+// until that work completes, so a new stream cannot alias it meanwhile.)
+// Rounds 1-3 recorded an event per release so that any stream could take
+// any slot: that marker packet idled the queue ~5 us before the next
 // call's kernel (1 x 256 MiB 54.7 -> 49.9 us per call without it; also with
 // the event carried by the kernel launch itself, hipExtLaunchKernel, 4.6 us:
 // profiles/r04/pool_event/).  With no free slot of the stream's own or
@@ -187,27 +188,28 @@ struct Scratch {
     int get(size_t bytes)
     {
         hipStreamCaptureStatus cs = hipStreamCaptureStatusActive;
-        const hipStream_t sid = s;
         if (ctx->pool_ready && hipStreamIsCapturing(s, &cs) == hipSuccess && cs == hipStreamCaptureStatusNone) {
             pthread_mutex_lock(&ctx->pool_lock);
-            // smallest free slot of this stream (or unowned) that fits, else the largest
-            int fit = -1, grow = -1;
+            // free slots of this stream first, then unowned ones: the smallest
+            // that fits, else the largest (grown)
+            int fit[2] = {-1, -1}, grow[2] = {-1, -1};
             for (int i = 0; i < NPOOL; i++) {
                 const priskv_crc_pool_slot &q = slots[i];
-                if (q.busy || (q.homed && q.home != sid))
+                if (q.busy || (q.homed && q.home != s))
                     continue;
+                const int o = q.homed ? 0 : 1;
                 if (q.size >= bytes) {
-                    if (fit < 0 || q.size < slots[fit].size)
-                        fit = i;
-                } else if (grow < 0 || q.size > slots[grow].size) {
-                    grow = i;
+                    if (fit[o] < 0 || q.size < slots[fit[o]].size)
+                        fit[o] = i;
+                } else if (grow[o] < 0 || q.size > slots[grow[o]].size) {
+                    grow[o] = i;
                 }
             }
-            const int k = fit >= 0 ? fit : grow;
+            const int k = fit[0] >= 0 ? fit[0] : fit[1] >= 0 ? fit[1] : grow[0] >= 0 ? grow[0] : grow[1];
             if (k >= 0) {
                 slots[k].busy = 1;
                 slots[k].homed = 1;
-                slots[k].home = sid;
+                slots[k].home = s;
             }
             pthread_mutex_unlock(&ctx->pool_lock);
             if (k >= 0) {
