@@ -444,7 +444,8 @@ constexpr Plan kPlans[NPLANS] = {
 // instead of three, +0.4-0.5 % at 4 GiB on every one of 6 allocations on two
 // boxes (same process, profiles/r04/nbuf4k/), while 256 MiB calls are level
 // to 2 % slower (a longer pipeline fill); round 2 measured 4 deep -0.9 % at
-// 4 GiB on round 2's code
+// 4 GiB on round 2's code.  5 and 6 deep: level (630.4 / 629.7 / 631.4 us
+// per 4 GiB call, medians of 5, profiles/r04/nbuf4k/nbuf_4_5_6_ab.jsonl)
 constexpr uint64_t kDeep4kBlocks = 1ull << 18; // 1 GiB
 
 int plan_for(uint32_t bs, uint64_t nblocks = 0)
