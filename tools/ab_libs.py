@@ -54,7 +54,11 @@ CASES = [("ranges 1x256MiB", 1, 256 << 20, 0), ("ranges 32x1MiB", 32, 1 << 20, (
          ("blocks 1x256MiB", 1, 256 << 20, 0), ("blocks 16x16MiB", 16, 16 << 20, 0),
          ("blocks 65536x4KiB", 65536, 4096, 0), ("blocks 4096x64KiB", 4096, 65536, 0),
          ("blocks 1024x1MiB", 1024, 1 << 20, 0), ("blocks 4096x1MiB", 4096, 1 << 20, 0),
-         ("blocks 1Mix4KiB", 1 << 20, 4096, 0)]
+         ("blocks 1Mix4KiB", 1 << 20, 4096, 0),
+         # odd sizes (the stride kernel), ~4 GiB per call
+         ("blocks odd4097", 1000000, 4097, 0), ("blocks odd4095", 1000000, 4095, 0),
+         ("blocks odd1000", 4000000, 1000, 0), ("blocks odd2047", 2000000, 2047, 0),
+         ("blocks odd8193", 500000, 8193, 0), ("blocks odd100", 40000000, 100, 0)]
 # PrisKV-shaped scattered values (tools/values_bench.py extents(): 1-4 blocks,
 # ragged ends, random blocks of the region)
 import numpy as np  # noqa: E402
