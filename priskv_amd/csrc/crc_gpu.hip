@@ -530,6 +530,15 @@ uint32_t tile_groups(const priskv_crc_ctx *ctx, uint64_t ngroups, uint64_t gstri
     return t ? (uint32_t)(t < (1u << 20) ? t : (1u << 20)) : 1u;
 }
 
+// the XCD weights of a split-mode launch over n units: from 32 units per wave
+uint32_t split_units_xw(const priskv_crc_ctx *ctx, int p, uint64_t n)
+{
+    const uint64_t max_wgs = (uint64_t)ctx->num_cus * ctx->plan_wgs_per_cu[p];
+    const uint64_t want = (n + kWaves - 1) / kWaves;
+    const uint64_t grid = want < max_wgs ? want : max_wgs;
+    return n >= 32ull * grid * kWaves ? ctx->plan_xw[p] : 0u;
+}
+
 // stride: bytes from block to block (0: bs; more for the head-split bodies).
 // split > 1: the split mode (ngroups = blocks; cnt / xacc: zeroed scratch of
 // ngroups words each, left zero), one launch
@@ -551,7 +560,7 @@ int launch_plan(const priskv_crc_ctx *ctx, int p, const uint8_t *base, uint64_t 
         uint64_t n = ngroups * split;
         const uint64_t want = (n + kWaves - 1) / kWaves;
         const uint32_t grid = (uint32_t)(want < max_wgs ? want : max_wgs);
-        uint32_t xw = n >= 32ull * grid * kWaves ? ctx->plan_xw[p] : 0u, tile = 0;
+        uint32_t xw = split_units_xw(ctx, p, n), tile = 0;
         void *args[] = {(void *)&base, (void *)&n,    (void *)&bs,    (void *)&img,   (void *)&fold,
                         (void *)&out,  (void *)&xw,   (void *)&tile,  (void *)&stride, (void *)&split,
                         (void *)&zp,   (void *)&cnt,  (void *)&xacc};
@@ -640,17 +649,25 @@ uint32_t split_for(const priskv_crc_ctx *ctx, uint64_t nblocks, uint32_t bs)
 // same split mode instead of segments + a combine kernel or the fused
 // kernel, with units down to one 4 KiB chunk, and on the 3-deep plan that
 // requests its first chunks before the tables (the 4 KiB plan's edge at
-// small calls: DESIGN §6).  1 = not applicable (then segments as before).
+// small calls: DESIGN §6).  Units aim at kSplitUnitsPerWave per wave (the
+// XCD weights apply from there) and are accepted from kSplitFewMinPerWave:
+// 32 MiB to 256 MiB batches (512 x 64 KiB, 100 x 1 MiB, 1000 x 128 KiB,
+// 200 x 512 KiB, 1500 x 64 KiB) then run 13-34 % faster than through
+// segments + combine (profiles/r04/split/split_few_units_ab.jsonl), while
+// larger ones keep their 32 units (aiming lower, at 4-16 per wave, cost
+// 1 x 256 MiB 5 %: split_few_upw_sweep.jsonl).  1 = not applicable (then
+// segments as before).
+constexpr uint64_t kSplitFewMinPerWave = 4;
+
 uint32_t split_few(const priskv_crc_ctx *ctx, uint64_t nblocks, uint32_t bs)
 {
     if (!ctx->split || bs % 4096 != 0)
         return 1;
-    const uint64_t want =
-        kSplitUnitsPerWave * (uint64_t)ctx->num_cus * ctx->plan_wgs_per_cu[PLAN_SPLIT_DEEP] * kWaves;
+    const uint64_t waves = (uint64_t)ctx->num_cus * ctx->plan_wgs_per_cu[PLAN_SPLIT_DEEP] * kWaves;
     uint32_t S = 1;
-    while (nblocks * S < want && (bs / 4096) % (2 * S) == 0)
+    while (nblocks * S < kSplitUnitsPerWave * waves && (bs / 4096) % (2 * S) == 0)
         S *= 2;
-    return nblocks * S >= want ? S : 1;
+    return nblocks * S >= kSplitFewMinPerWave * waves ? S : 1;
 }
 
 int launch_split(const priskv_crc_ctx *ctx, int p, const uint8_t *base, uint64_t nblocks, uint32_t bs, uint32_t S,
@@ -1294,7 +1311,8 @@ int priskv_crc32_blocks_plan(const priskv_crc_ctx *ctx, const void *d_base, uint
         }
     } else if (path == PATH_ROWS && segments_for(ctx, nblocks, block_size) > 1 &&
                split_few(ctx, nblocks, block_size) > 1) {
-        const uint32_t sf = split_few(ctx, nblocks, block_size), xw = ctx->plan_xw[PLAN_SPLIT_DEEP];
+        const uint32_t sf = split_few(ctx, nblocks, block_size);
+        const uint32_t xw = split_units_xw(ctx, PLAN_SPLIT_DEEP, nblocks * sf);
         w = snprintf(buf, len,
                      "crc_rows_kernel<G=64,CH=4,NBUF=3,nt,nibble-fold%s,first chunks before the tables,"
                      "split %u units of %u B per block%s",

@@ -1079,10 +1079,12 @@ def test_full_config_1M_x_4K(torch_cuda, ctx):
 # 1 MiB gives fewer units per wave than units per block (waves whose whole
 # range lies inside one block)
 _SPLIT_CASES = [(1 << 20, 1900), (1 << 20, 4096), (512 << 10, 4000), (256 << 10, 6000), (1 << 20, 2048),
-                # few large blocks: the 3-deep plan, units down to one 4 KiB chunk
+                # few large blocks: the 3-deep plan, units down to one 4 KiB chunk, 32 per wave
                 (256 << 20, 1), (16 << 20, 16), (1 << 20, 1000), (32 << 20, 8),
-                # ... but not when they cannot be cut into 32 units per wave (the fused kernel)
-                (12 << 20, 3)]
+                # ... or from 4 per wave, without the XCD weights (32-256 MiB batches)
+                (64 << 10, 512), (128 << 10, 1000), (1 << 20, 100), (12 << 20, 3),
+                # ... but not below 4 units per wave (the fused kernel)
+                (4 << 20, 3), (12 << 20, 1)]
 
 
 def test_verify_graph_capture(torch_cuda, ctx):
@@ -1172,7 +1174,10 @@ def test_rows_split_mode(torch_cuda, ctx, bs, nb):
     xcd = "xcd-weighted" in ctx.blocks_plan(view.data_ptr(), 1 << 20, 4096)  # the probe saw round-robin XCDs
     waves = torch.cuda.get_device_properties(0).multi_processor_count * 8
     unbal = nb * 10 < 9 * waves
-    few = unbal and nb * (bs // 4096) >= 32 * waves  # unbalanced and 32 units of >= 4 KiB per wave
+    S = 1  # units per block: power-of-two cuts of whole 4 KiB chunks, toward 32 per wave
+    while nb * S < 32 * waves and (bs // 4096) % (2 * S) == 0:
+        S *= 2
+    few = unbal and nb * S >= 4 * waves  # unbalanced, and at least 4 units per wave
     assert ("split" in plan) == (few or (xcd and not unbal)), plan
     assert ("few large blocks" in plan) == few, plan
     want = O.crc32_blocks(view.cpu().numpy(), bs, nthreads=16)

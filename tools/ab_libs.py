@@ -58,7 +58,17 @@ CASES = [("ranges 1x256MiB", 1, 256 << 20, 0), ("ranges 32x1MiB", 32, 1 << 20, (
          # odd sizes (the stride kernel), ~4 GiB per call
          ("blocks odd4097", 1000000, 4097, 0), ("blocks odd4095", 1000000, 4095, 0),
          ("blocks odd1000", 4000000, 1000, 0), ("blocks odd2047", 2000000, 2047, 0),
-         ("blocks odd8193", 500000, 8193, 0), ("blocks odd100", 40000000, 100, 0)]
+         ("blocks odd8193", 500000, 8193, 0), ("blocks odd100", 40000000, 100, 0),
+         # 32 MiB calls: few large values / blocks against the rows kernel
+         ("small32 ranges 32x1MiB", 32, 1 << 20, 1 << 20), ("small32 ranges 16x2MiB", 16, 2 << 20, 2 << 20),
+         ("small32 blocks 32x1MiB", 32, 1 << 20, 0), ("small32 blocks 8192x4KiB", 8192, 4096, 0),
+         ("small32 blocks 512x64KiB", 512, 65536, 0),
+         # unbalanced batches below the split-few size: rows + combine (blocks) against the fused kernel (ranges)
+         ("mid ranges 512x64KiB", 512, 65536, 65536), ("mid blocks 512x64KiB", 512, 65536, 0),
+         ("mid ranges 100x1MiB", 100, 1 << 20, 1 << 20), ("mid blocks 100x1MiB", 100, 1 << 20, 0),
+         ("mid ranges 1000x128KiB", 1000, 128 << 10, 128 << 10), ("mid blocks 1000x128KiB", 1000, 128 << 10, 0),
+         ("mid ranges 200x512KiB", 200, 512 << 10, 512 << 10), ("mid blocks 200x512KiB", 200, 512 << 10, 0),
+         ("mid ranges 1500x64KiB", 1500, 65536, 65536), ("mid blocks 1500x64KiB", 1500, 65536, 0)]
 # PrisKV-shaped scattered values (tools/values_bench.py extents(): 1-4 blocks,
 # ragged ends, random blocks of the region)
 import numpy as np  # noqa: E402
@@ -90,7 +100,7 @@ for r in range(ROUNDS):
             sp = s.cuda_stream
 
             def call():
-                if name.startswith("ranges"):
+                if name.split()[-2] == "ranges" or name.startswith("ranges"):
                     rc = L.priskv_crc32_ranges_dev(h, region.data_ptr(), offs.data_ptr(), lens.data_ptr(), n,
                                                    out.data_ptr(), sp)
                 else:
