@@ -115,6 +115,7 @@ for r in range(ROUNDS):
             e1.record(s)
             e1.synchronize()
             got = out.cpu().numpy().tobytes()
-            assert ref.setdefault(name, got) == got, (name, tag)  # A and B agree bit for bit
+            if "--nocheck" not in sys.argv:  # (--nocheck: timing-only probes of deliberately wrong builds)
+                assert ref.setdefault(name, got) == got, (name, tag)  # A and B agree bit for bit
             print(json.dumps({"round": r, "case": name, "variant": tag, "us_per_call": round(e0.elapsed_time(e1) / 50 * 1e3, 2)}),
                   flush=True)
