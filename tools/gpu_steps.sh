@@ -24,6 +24,7 @@
 #   pmc:C1+C2[:A,B,...]   one rocprofv3 --pmc pass (counters C1 C2 ...) over bench.py A B ...
 #   pmcpy:C1+C2:SCRIPT[:A,B]  one --pmc pass over python tools/SCRIPT A B ...
 #   pmclib:C1+C2:ARGS     one --pmc pass over tools/lib_timing ARGS (no torch in the process)
+#   pmclibenv:VAR=V:C1+C2:ARGS  the same with one environment variable exported first
 #   probe:ENV2:ARGS       tools/alloc_probe ARGS, second context with ENV2 (A/B, same allocations)
 #   pmcprobe:C1+C2:ARGS   one --pmc pass over tools/alloc_probe ARGS
 #   ktracelib:ARGS        rocprofv3 --kernel-trace --stats over tools/lib_timing ARGS
@@ -143,7 +144,17 @@ for step in "$@"; do
         ctrs=${arg%%:*}
         largs=""
         [[ "$arg" == *:* ]] && largs=${arg#*:}
-        (cd /tmp && export TMPDIR=/tmp &&
+        (cd /tmp && export TMPDIR=/tmp LIB_TIMING_RAMP=20 &&
+            timeout -s KILL 120 rocprofv3 --pmc ${ctrs//+/ } -d "$O/pmclib_$n" -o run --output-format csv \
+                -- "$R/tools/lib_timing" ${largs//,/ } > "$O/pmclib_$n.out" 2> "$O/pmclib_$n.err")
+        ;;
+    pmclibenv)
+        kv=${arg%%:*}
+        rest=${arg#*:}
+        ctrs=${rest%%:*}
+        largs=""
+        [[ "$rest" == *:* ]] && largs=${rest#*:}
+        (cd /tmp && export TMPDIR=/tmp LIB_TIMING_RAMP=20 && export "$kv" &&
             timeout -s KILL 120 rocprofv3 --pmc ${ctrs//+/ } -d "$O/pmclib_$n" -o run --output-format csv \
                 -- "$R/tools/lib_timing" ${largs//,/ } > "$O/pmclib_$n.out" 2> "$O/pmclib_$n.err")
         ;;

@@ -2,6 +2,9 @@
 // with plain hipMalloc'd memory and no torch in the process (tools only):
 // separates "the kernel" from "bench.py's process" when their numbers differ.
 // Usage: lib_timing [block_size] [nblocks] [launches] [rounds]
+// LIB_TIMING_ROOF=1: time priskv_crc_read_roof_dev (the plan's loads, no
+// hashing) instead; LIB_TIMING_RAMP=N: N ramp launches (default 400; fewer
+// under rocprofv3 --pmc, which serialises every dispatch).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -44,14 +47,19 @@ int main(int argc, char **argv)
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
-    for (int i = 0; i < 400; i++) // ramp
-        priskv_crc32_blocks_dev(ctx, d, nb, bs, o, s);
+    const bool roof = getenv("LIB_TIMING_ROOF") && atoi(getenv("LIB_TIMING_ROOF"));
+    const int ramp = getenv("LIB_TIMING_RAMP") ? atoi(getenv("LIB_TIMING_RAMP")) : 400;
+    auto call = [&]() {
+        return roof ? priskv_crc_read_roof_dev(ctx, d, nb, bs, o, s) : priskv_crc32_blocks_dev(ctx, d, nb, bs, o, s);
+    };
+    for (int i = 0; i < ramp; i++) // ramp
+        call();
     CK(hipStreamSynchronize(s));
     std::vector<float> ms;
     for (int r = 0; r < rounds; r++) {
         CK(hipEventRecord(e0, s));
         for (int i = 0; i < k; i++)
-            if (priskv_crc32_blocks_dev(ctx, d, nb, bs, o, s))
+            if (call())
                 return 3;
         CK(hipEventRecord(e1, s));
         CK(hipEventSynchronize(e1));
@@ -61,9 +69,9 @@ int main(int argc, char **argv)
     }
     std::sort(ms.begin(), ms.end());
     const double alg = (double)nb * (bs + 4);
-    printf("{\"tool\": \"lib_timing\", \"block_size\": %u, \"nblocks\": %llu, \"plan\": \"%s\", \"launches\": %d, "
+    printf("{\"tool\": \"lib_timing\", \"roof\": %d, \"block_size\": %u, \"nblocks\": %llu, \"plan\": \"%s\", \"launches\": %d, "
            "\"median_ms\": %.4f, \"min_ms\": %.4f, \"max_ms\": %.4f, \"TBps_median\": %.3f}\n",
-           bs, (unsigned long long)nb, plan, k, ms[ms.size() / 2], ms[0], ms.back(), alg / ms[ms.size() / 2] / 1e9);
+           (int)roof, bs, (unsigned long long)nb, plan, k, ms[ms.size() / 2], ms[0], ms.back(), alg / ms[ms.size() / 2] / 1e9);
     priskv_crc_ctx_destroy(ctx);
     return 0;
 }
