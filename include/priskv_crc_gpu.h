@@ -54,6 +54,15 @@ int priskv_crc_ctx_create(int device, priskv_crc_ctx **out);
 void priskv_crc_ctx_destroy(priskv_crc_ctx *ctx);
 int priskv_crc_ctx_device(const priskv_crc_ctx *ctx);
 
+/* Hand the scratch-pool slots `stream` owns back to the context's pool
+ * (a slot belongs to the first stream that takes it; hipStreamPerThread's
+ * belong to the calling thread).  Waits for the stream's work first.  Call
+ * it before destroying a stream that ran *_dev calls -- or from a thread
+ * about to exit that used hipStreamPerThread -- while no other thread
+ * submits to that stream.  Optional: a stream that finds the pool full also
+ * takes over slots of streams that have no work left.  0 / -EINVAL / -EIO. */
+int priskv_crc_stream_release(const priskv_crc_ctx *ctx, void *stream);
+
 /* Device-resident batch: d_base -> nblocks * block_size bytes of device
  * memory; d_out -> uint32_t[nblocks] of device memory.  d_out[i] =
  * priskv_crc32(d_base + i*block_size, block_size).  Asynchronous on `stream`.
@@ -205,17 +214,23 @@ int priskv_crc32_blocks_plan(const priskv_crc_ctx *ctx, const void *d_base, uint
                              char *buf, uint64_t len);
 
 /* Diagnostic: the read roof of the CRC kernel's access pattern.  Reads
- * nblocks x block_size bytes at d_base with exactly the loads, per-wave
- * ranges, pipeline depth and XCD split crc_rows_kernel uses for this block
- * size (block_size a multiple of 4 KiB, d_base 16-byte aligned), without
- * hashing; each wave XORs the XOR of the 32-bit words it read into one entry
- * of d_sink (nblocks uint32 entries; which entries is unspecified), so with
- * a zeroed sink the XOR of all its entries is the XOR of the batch's words.  Timing it beside
- * priskv_crc32_blocks_dev on the same region gives the fraction of what HBM
- * delivers for this pattern that the CRC reaches.  Asynchronous on stream;
- * 0 or -EINVAL / -ENODEV / -EIO. */
+ * nblocks x block_size bytes at d_base with the loads, per-wave ranges and
+ * XCD split crc_rows_kernel uses for this block size (block_size a multiple
+ * of 4 KiB, d_base 16-byte aligned), without hashing.  variant 0 runs in the
+ * CRC plan's own pipeline depth and occupancy; variants 1 ..
+ * PRISKV_CRC_ROOF_VARIANTS - 1 in 2, 2, 3, 3, 4, 4 chunks in flight at one /
+ * two 8-wave workgroups per CU, so the best variant bounds what HBM gives
+ * this pattern.  d_sink: PRISKV_CRC_ROOF_SINK_WORDS uint32 entries; launched
+ * wave w stores the XOR of the 32-bit words it read in d_sink[w] (plain
+ * stores, other entries untouched), so over a zeroed sink the XOR of all
+ * entries is the XOR of the batch's words.  Timing it beside
+ * priskv_crc32_blocks_dev on the same region gives the fraction of this
+ * pattern's roof the CRC reaches.  Asynchronous on stream; 0, or -EINVAL
+ * (also for a batch of more than 2^31 chunks per wave) / -ENODEV / -EIO. */
+#define PRISKV_CRC_ROOF_VARIANTS 7
+#define PRISKV_CRC_ROOF_SINK_WORDS 8192
 int priskv_crc_read_roof_dev(const priskv_crc_ctx *ctx, const void *d_base, uint64_t nblocks,
-                             uint32_t block_size, uint32_t *d_sink, void *stream);
+                             uint32_t block_size, uint32_t variant, uint32_t *d_sink, void *stream);
 
 const char *priskv_crc_version(void);
 

@@ -31,6 +31,10 @@ PATH_NAMES = {PATH_ROWS: "rows", PATH_EXTENTS: "extents", PATH_SMALL: "small", P
 
 _lib: Optional[ctypes.CDLL] = None
 
+# include/priskv_crc_gpu.h: read-roof variants and sink size
+ROOF_VARIANTS = 7
+ROOF_SINK_WORDS = 8192
+
 # (name, restype, argtypes) for every symbol the two headers declare
 _C = ctypes
 SIGNATURES = [
@@ -38,6 +42,7 @@ SIGNATURES = [
     ("priskv_crc_ctx_create", _C.c_int, [_C.c_int, _C.POINTER(_C.c_void_p)]),
     ("priskv_crc_ctx_destroy", None, [_C.c_void_p]),
     ("priskv_crc_ctx_device", _C.c_int, [_C.c_void_p]),
+    ("priskv_crc_stream_release", _C.c_int, [_C.c_void_p, _C.c_void_p]),
     ("priskv_crc32_blocks_dev", _C.c_int,
      [_C.c_void_p, _C.c_void_p, _C.c_uint64, _C.c_uint32, _C.c_void_p, _C.c_void_p]),
     ("priskv_crc32_ranges_dev", _C.c_int,
@@ -70,7 +75,7 @@ SIGNATURES = [
     ("priskv_crc32_blocks_plan", _C.c_int,
      [_C.c_void_p, _C.c_void_p, _C.c_uint64, _C.c_uint32, _C.c_char_p, _C.c_uint64]),
     ("priskv_crc_read_roof_dev", _C.c_int,
-     [_C.c_void_p, _C.c_void_p, _C.c_uint64, _C.c_uint32, _C.c_void_p, _C.c_void_p]),
+     [_C.c_void_p, _C.c_void_p, _C.c_uint64, _C.c_uint32, _C.c_uint32, _C.c_void_p, _C.c_void_p]),
     ("priskv_crc_version", _C.c_char_p, []),
 ]
 
@@ -196,6 +201,12 @@ class CrcContext:
     def handle(self) -> ctypes.c_void_p:
         return self._h
 
+    def stream_release(self, stream) -> None:
+        """Hand `stream`'s scratch-pool slots back (priskv_crc_stream_release;
+        waits for the stream).  Call before destroying a stream that ran
+        *_dev calls, while no other thread submits to it."""
+        _check(lib().priskv_crc_stream_release(self._h, _stream_ptr(stream)), "priskv_crc_stream_release")
+
     def blocks_plan(self, region_ptr: int, nblocks: int, block_size: int) -> str:
         """The kernel plan blocks_dev would launch (priskv_crc32_blocks_plan)."""
         buf = ctypes.create_string_buffer(256)
@@ -267,15 +278,19 @@ class CrcContext:
                                                   word_offset, _stream_ptr(stream)),
                "priskv_crc_fill_splitmix_dev")
 
-    def read_roof_dev(self, region, block_size: int, sink, stream=None, nblocks: Optional[int] = None) -> None:
+    def read_roof_dev(self, region, block_size: int, sink, stream=None, nblocks: Optional[int] = None,
+                      variant: int = 0) -> None:
         """Diagnostic read roof of the CRC kernel's access pattern over `region`
-        (priskv_crc_read_roof_dev; sink: >= nblocks 4-byte entries)."""
+        (priskv_crc_read_roof_dev): variant 0 in the CRC plan's own pipeline
+        depth and occupancy, 1 .. ROOF_VARIANTS - 1 in others; sink:
+        ROOF_SINK_WORDS 4-byte entries, one per launched wave."""
         nbytes = region.numel() * region.element_size()
         n = nbytes // block_size if nblocks is None else nblocks
-        if n * block_size > nbytes or sink.numel() < n or sink.element_size() != 4 or not sink.is_contiguous():
-            raise ValueError("nblocks * block_size must fit the region and sink hold >= nblocks 4-byte entries")
+        if (n * block_size > nbytes or sink.numel() < ROOF_SINK_WORDS or sink.element_size() != 4
+                or not sink.is_contiguous()):
+            raise ValueError("nblocks * block_size must fit the region and sink hold ROOF_SINK_WORDS 4-byte entries")
         _device_args(region, sink)
-        _check(lib().priskv_crc_read_roof_dev(self._h, region.data_ptr(), n, block_size, sink.data_ptr(),
+        _check(lib().priskv_crc_read_roof_dev(self._h, region.data_ptr(), n, block_size, variant, sink.data_ptr(),
                                               _stream_ptr(stream)), "priskv_crc_read_roof_dev")
 
     # ---- host-resident (streamed over PCIe)

@@ -37,6 +37,8 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <tuple>
+#include <type_traits>
 #include <vector>
 
 #include "../../include/priskv_crc_gpu.h"
@@ -58,8 +60,9 @@ struct priskv_crc_pool_slot {
     void *p;
     size_t size;
     hipStream_t home; // the one stream that uses the slot
-    int homed;               // home is set (the slot has been taken once)
-    int busy;                // taken by a call in flight on the host
+    pthread_t tid;    // home == hipStreamPerThread: the host thread whose stream it is
+    int homed;        // home is set (the slot has been taken once)
+    int busy;         // taken by a call in flight on the host
 };
 
 struct priskv_crc_ctx {
@@ -134,6 +137,24 @@ struct DevGuard {
     }
 };
 
+inline int herr(hipError_t e);
+
+// hipLaunchKernel with the kernel's own parameter types.  Its return value is
+// this launch's status; hipGetLastError after hipLaunchKernelGGL would also
+// report an earlier, unrelated failure on the calling thread.
+template <typename... P, typename... A>
+int launch_k(void (*k)(P...), dim3 grid, dim3 block, hipStream_t s, A &&...a)
+{
+    static_assert(sizeof...(P) == sizeof...(A), "one argument per kernel parameter");
+    std::tuple<std::decay_t<P>...> t(static_cast<std::decay_t<P>>(a)...);
+    return std::apply(
+        [&](auto &...v) {
+            void *args[] = {(void *)&v...};
+            return herr(hipLaunchKernel(reinterpret_cast<const void *>(k), grid, block, args, 0, s));
+        },
+        t);
+}
+
 inline int herr(hipError_t e)
 {
     if (e == hipSuccess)
@@ -154,6 +175,12 @@ inline int herr(hipError_t e)
 // stream order alone puts its previous use first -- no event.  (A handle
 // stays taken while its stream has work: a destroyed stream's object lives
 // until that work completes, so a new stream cannot alias it meanwhile.)
+// hipStreamPerThread names a different stream on every host thread, so its
+// slots belong to (handle, thread).  A stream that finds no slot of its own
+// and none unowned takes over a free slot whose stream has no work left
+// (hipStreamQuery), so slots of streams a server has destroyed return to the
+// pool; priskv_crc_stream_release hands a stream's slots back explicitly
+// (the only way for a hipStreamPerThread thread that is about to exit).
 // Rounds 1-3 recorded an event per release so that any stream could take
 // any slot: that marker packet idled the queue ~5 us before the next
 // call's kernel (1 x 256 MiB 54.7 -> 49.9 us per call without it; also with
@@ -182,20 +209,26 @@ struct Scratch {
     {
         const uint64_t nw = bytes / 4;
         const uint32_t grid = (uint32_t)(nw / 256 + 1 < 1024 ? nw / 256 + 1 : 1024);
-        hipLaunchKernelGGL(crc_zero_kernel, dim3(grid), dim3(256), 0, s, static_cast<uint32_t *>(q), nw);
-        return herr(hipGetLastError());
+        return launch_k(crc_zero_kernel, dim3(grid), dim3(256), s, static_cast<uint32_t *>(q), nw);
     }
     int get(size_t bytes)
     {
         hipStreamCaptureStatus cs = hipStreamCaptureStatusActive;
         if (ctx->pool_ready && hipStreamIsCapturing(s, &cs) == hipSuccess && cs == hipStreamCaptureStatusNone) {
+            // hipStreamPerThread is one handle that names a different stream
+            // on every host thread: its slots belong to (handle, thread)
+            const bool pt = s == hipStreamPerThread;
+            const pthread_t self = pthread_self();
+            auto own = [&](const priskv_crc_pool_slot &q) {
+                return q.home == s && (!pt || pthread_equal(q.tid, self));
+            };
             pthread_mutex_lock(&ctx->pool_lock);
             // free slots of this stream first, then unowned ones: the smallest
             // that fits, else the largest (grown)
             int fit[2] = {-1, -1}, grow[2] = {-1, -1};
             for (int i = 0; i < NPOOL; i++) {
                 const priskv_crc_pool_slot &q = slots[i];
-                if (q.busy || (q.homed && q.home != s))
+                if (q.busy || (q.homed && !own(q)))
                     continue;
                 const int o = q.homed ? 0 : 1;
                 if (q.size >= bytes) {
@@ -205,11 +238,23 @@ struct Scratch {
                     grow[o] = i;
                 }
             }
-            const int k = fit[0] >= 0 ? fit[0] : fit[1] >= 0 ? fit[1] : grow[0] >= 0 ? grow[0] : grow[1];
+            int k = fit[0] >= 0 ? fit[0] : fit[1] >= 0 ? fit[1] : grow[0] >= 0 ? grow[0] : grow[1];
+            // none: take over a free slot of another stream that has no work
+            // left (every use of the slot is complete; a destroyed stream's
+            // handle no longer names a live stream).  hipStreamPerThread homes
+            // cannot be queried from here and stay with their thread.
+            for (int i = 0; k < 0 && i < NPOOL; i++) {
+                const priskv_crc_pool_slot &q = slots[i];
+                if (q.busy || !q.homed || q.home == hipStreamPerThread)
+                    continue;
+                if (hipStreamQuery(q.home) != hipErrorNotReady)
+                    k = i;
+            }
             if (k >= 0) {
                 slots[k].busy = 1;
                 slots[k].homed = 1;
                 slots[k].home = s;
+                slots[k].tid = self;
             }
             pthread_mutex_unlock(&ctx->pool_lock);
             if (k >= 0) {
@@ -220,7 +265,7 @@ struct Scratch {
                     while (cap < bytes)
                         cap *= 2;
                     if (q.p)
-                        rc = herr(hipFreeAsync(q.p, s)); // after the slot's last use: same stream
+                        rc = herr(hipFreeAsync(q.p, s)); // after the slot's last use: same stream, or none pending
                     q.p = nullptr;
                     q.size = 0;
                     if (!rc && !(rc = herr(hipMallocAsync(&q.p, cap, s))))
@@ -295,9 +340,8 @@ int launch_generic(const priskv_crc_ctx *ctx, const uint8_t *base, uint64_t n, u
     uint32_t grid = (uint32_t)(want < (uint64_t)ctx->num_cus * 8 ? want : (uint64_t)ctx->num_cus * 8);
     if (grid == 0)
         grid = 1;
-    hipLaunchKernelGGL(crc_generic_kernel, dim3(grid), dim3(256), 0, s, base, n, stride, len_const, offs,
-                       lens, ctx->d_sarwate, out);
-    return herr(hipGetLastError());
+    return launch_k(crc_generic_kernel, dim3(grid), dim3(256), s, base, n, stride, len_const, offs, lens,
+                    ctx->d_sarwate, out);
 }
 
 constexpr int kNbuf = 2;  // register pipeline depth (chunks) of the extents kernel
@@ -380,9 +424,8 @@ int launch_extents(const priskv_crc_ctx *ctx, const uint8_t *base, uint64_t n, c
         if (int rc = scr.get(ntiles * sizeof(uint32_t)))
             return rc;
         uint32_t *tiles = static_cast<uint32_t *>(scr.p);
-        hipLaunchKernelGGL(crc_ext_cost_kernel, dim3((uint32_t)((ntiles + 3) / 4)), dim3(256), 0, s, lens, n, tiles,
-                           ntiles);
-        int rc = herr(hipGetLastError());
+        int rc = launch_k(crc_ext_cost_kernel, dim3((uint32_t)((ntiles + 3) / 4)), dim3(256), s, lens, n, tiles,
+                          ntiles);
         if (!rc)
             rc = launch_ext_kernel(ctx, false, false, true, s, abase, n, offs, lens, shift, stride, len_const, out,
                                    tiles, nullptr, nullptr, nullptr);
@@ -804,9 +847,8 @@ int launch_extents_seg(const priskv_crc_ctx *ctx, const uint8_t *base, uint64_t 
     uint32_t *prefix = reinterpret_cast<uint32_t *>(scr);
     uint8_t *shifts = scr + off_shift;
     uint32_t *sub = reinterpret_cast<uint32_t *>(scr + off_sub);
-    hipLaunchKernelGGL(crc_seg_plan_kernel, dim3(1), dim3(kSegPlanThreads), 0, s, offs ? lens : nullptr, len_const, n,
-                       (uint32_t)target, prefix, shifts);
-    int rc = herr(hipGetLastError());
+    int rc = launch_k(crc_seg_plan_kernel, dim3(1), dim3(kSegPlanThreads), s, offs ? lens : nullptr, len_const, n,
+                      (uint32_t)target, prefix, shifts);
     if (!rc) {
         const uint64_t sh = (uintptr_t)base & 15;
         rc = launch_ext_kernel(ctx, true, false, false, s, base - sh, n, offs, lens, sh, stride, len_const, out, prefix, shifts,
@@ -814,9 +856,8 @@ int launch_extents_seg(const priskv_crc_ctx *ctx, const uint8_t *base, uint64_t 
     }
     if (!rc) {
         const uint32_t grid = (uint32_t)n; // one workgroup per extent (n <= 16384)
-        hipLaunchKernelGGL(crc_seg_reduce_kernel, dim3(grid), dim3(kSegReduceThreads), 0, s, sub, prefix, shifts,
-                           offs ? lens : nullptr, len_const, ctx->d_zpow, n, out);
-        rc = herr(hipGetLastError());
+        rc = launch_k(crc_seg_reduce_kernel, dim3(grid), dim3(kSegReduceThreads), s, sub, prefix, shifts,
+                      offs ? lens : nullptr, len_const, ctx->d_zpow, n, out);
     }
     const int frc = sc.release();
     *used = true;
@@ -855,8 +896,7 @@ int launch_rows(const priskv_crc_ctx *ctx, const uint8_t *base, uint64_t nblocks
             prv_shift_columns(z.c[1 + b], (uint64_t)(bs / S) * r << b);
         const uint64_t want = (nblocks + 3) / 4; // one wave per block
         const uint32_t grid = (uint32_t)(want < (uint64_t)ctx->num_cus * 8 ? want : (uint64_t)ctx->num_cus * 8);
-        hipLaunchKernelGGL(crc_combine_segments_kernel, dim3(grid), dim3(256), 0, s, sub, nblocks, S, r, z, out);
-        rc = herr(hipGetLastError());
+        rc = launch_k(crc_combine_segments_kernel, dim3(grid), dim3(256), s, sub, nblocks, S, r, z, out);
     }
     const int frc = sc.release();
     return rc ? rc : frc;
@@ -918,8 +958,7 @@ int launch_head_split(const priskv_crc_ctx *ctx, const uint8_t *base, uint64_t n
     prv_shift_columns(z.c, body);
     const uint64_t want = (nblocks + 255) / 256;
     const uint32_t grid = (uint32_t)(want < (uint64_t)ctx->num_cus * 8 ? want : (uint64_t)ctx->num_cus * 8);
-    hipLaunchKernelGGL(crc_head_kernel, dim3(grid), dim3(256), 0, s, base, nblocks, bs, h, ctx->d_sarwate, z, out);
-    return herr(hipGetLastError());
+    return launch_k(crc_head_kernel, dim3(grid), dim3(256), s, base, nblocks, bs, h, ctx->d_sarwate, z, out);
 }
 
 // sub-KiB kernel for G = 1 << gl: no fold at G = 1 (a lane holds a whole
@@ -1183,8 +1222,6 @@ int launch_blocks(const priskv_crc_ctx *ctx, const uint8_t *base, uint64_t nbloc
             void *args[] = {(void *)&base, (void *)&nrows, (void *)&img, (void *)&fold, (void *)&out};
             if (int rc = herr(hipLaunchKernel(small_fn(gl, prio, bf), dim3(grid), dim3(64 * waves), args, 0, s)))
                 return rc;
-            if (int rc = herr(hipGetLastError()))
-                return rc;
         }
         const uint64_t head = nrows * per;
         if (head == nblocks)
@@ -1235,8 +1272,7 @@ int xcd_probe(priskv_crc_ctx *c, int *rr)
     int rc = herr(hipMalloc((void **)&d, sizeof(h)));
     if (rc)
         return rc;
-    hipLaunchKernelGGL(crc_xcd_probe_kernel, dim3(kProbeWgs), dim3(64), 0, c->aux, d);
-    if (!(rc = herr(hipGetLastError())) &&
+    if (!(rc = launch_k(crc_xcd_probe_kernel, dim3(kProbeWgs), dim3(64), c->aux, d)) &&
         !(rc = herr(hipMemcpyAsync(h, d, sizeof(h), hipMemcpyDeviceToHost, c->aux))))
         rc = herr(hipStreamSynchronize(c->aux));
     (void)hipFree(d);
@@ -1364,9 +1400,10 @@ int priskv_crc32_blocks_plan(const priskv_crc_ctx *ctx, const void *d_base, uint
 }
 
 int priskv_crc_read_roof_dev(const priskv_crc_ctx *ctx, const void *d_base, uint64_t nblocks, uint32_t block_size,
-                             uint32_t *d_sink, void *stream)
+                             uint32_t variant, uint32_t *d_sink, void *stream)
 {
-    if (!ctx || block_size == 0 || block_size % 4096 != 0 || ((uintptr_t)d_base & 15) != 0)
+    if (!ctx || block_size == 0 || block_size % 4096 != 0 || ((uintptr_t)d_base & 15) != 0 ||
+        variant >= PRISKV_CRC_ROOF_VARIANTS)
         return -EINVAL;
     if (nblocks == 0)
         return 0;
@@ -1375,44 +1412,39 @@ int priskv_crc_read_roof_dev(const priskv_crc_ctx *ctx, const void *d_base, uint
     DevGuard g(ctx->device);
     if (!g.ok)
         return -ENODEV;
-    // the plan the CRC kernel uses for this block size: its pipeline depth,
-    // its resident workgroups, its split mode (units of block_size / S) and
-    // its XCD weights (only with many units per wave, as launch_plan applies
-    // them); the roof reads units as blocks
+    // the plan the CRC kernel uses for this block size: its resident
+    // workgroups and pipeline depth (variant 0; variants 1-6: NBUF 2 / 3 / 4
+    // at one or two 8-wave workgroups per CU), its split mode (units of
+    // block_size / S) and its XCD weights (only with many units per wave, as
+    // launch_plan applies them); the roof reads units as blocks
     int p = plan_for(block_size, nblocks);
     uint32_t S = 1;
     if (segments_for(ctx, nblocks, block_size) == 1)
         S = split_for(ctx, nblocks, block_size);
     else if ((S = split_few(ctx, nblocks, block_size)) > 1)
         p = PLAN_SPLIT_DEEP;
-    const Plan &P = kPlans[p];
-    const uint64_t max_wgs = (uint64_t)ctx->num_cus * ctx->plan_wgs_per_cu[p];
+    const int nbuf = variant ? 2 + (int)(variant - 1) / 2 : kPlans[p].NBUF;
+    const uint64_t wgpc = variant ? 1 + (variant - 1) % 2 : (uint64_t)ctx->plan_wgs_per_cu[p];
+    const uint64_t max_wgs = (uint64_t)ctx->num_cus * wgpc;
     block_size /= S;
     nblocks *= S;
     const uint64_t cps = block_size / 4096;
-    const uint64_t cap = max_wgs * kWaves * ((1ull << 31) / cps - 1);
-    const uint8_t *base = static_cast<const uint8_t *>(d_base);
-    const void *fn = P.NBUF == 4   ? reinterpret_cast<const void *>(&crc_read_roof_kernel<4, 4, kAux>)
-                     : P.NBUF == 3 ? reinterpret_cast<const void *>(&crc_read_roof_kernel<4, 3, kAux>)
-                                   : reinterpret_cast<const void *>(&crc_read_roof_kernel<4, 2, kAux>);
-    for (uint64_t done = 0; done < nblocks;) {
-        uint64_t n = nblocks - done < cap ? nblocks - done : cap;
-        const uint64_t want = (n + kWaves - 1) / kWaves;
-        const uint32_t grid = (uint32_t)(want < max_wgs ? want : max_wgs);
-        const uint8_t *b = base + done * (uint64_t)block_size;
-        uint32_t *o = d_sink + done / S;
-        uint32_t bs = block_size;
-        uint32_t xw = n >= 32ull * grid * kWaves ? ctx->plan_xw[p] : 0u;
-        uint32_t ush = (uint32_t)log2u(S);
-        uint32_t tile = S == 1 ? tile_groups(ctx, n, bs) : 0u; // the CRC kernel's tiles (G = 64: a group is a block)
-        if (tile)
-            xw = 0;
-        void *args[] = {(void *)&b, (void *)&n, (void *)&bs, (void *)&o, (void *)&xw, (void *)&ush, (void *)&tile};
-        if (int rc = herr(hipLaunchKernel(fn, dim3(grid), dim3(kThreads), args, 0, (hipStream_t)stream)))
-            return rc;
-        done += n;
-    }
-    return 0;
+    const uint64_t want = (nblocks + kWaves - 1) / kWaves;
+    const uint32_t grid = (uint32_t)(want < max_wgs ? want : max_wgs);
+    // one launch (a wave's chunk count is 32-bit) and one sink slot per wave
+    if ((uint64_t)grid * kWaves > PRISKV_CRC_ROOF_SINK_WORDS || (nblocks + grid * kWaves - 1) / (grid * kWaves) * cps >= (1ull << 31))
+        return -EINVAL;
+    const uint8_t *b = static_cast<const uint8_t *>(d_base);
+    uint32_t bs = block_size;
+    uint32_t xw = nblocks >= 32ull * grid * kWaves ? ctx->plan_xw[p] : 0u;
+    uint32_t tile = S == 1 ? tile_groups(ctx, nblocks, bs) : 0u; // the CRC kernel's tiles (G = 64: a group is a block)
+    if (tile)
+        xw = 0;
+    const void *fn = nbuf == 4   ? reinterpret_cast<const void *>(&crc_read_roof_kernel<4, 4, kAux>)
+                     : nbuf == 3 ? reinterpret_cast<const void *>(&crc_read_roof_kernel<4, 3, kAux>)
+                                 : reinterpret_cast<const void *>(&crc_read_roof_kernel<4, 2, kAux>);
+    void *args[] = {(void *)&b, (void *)&nblocks, (void *)&bs, (void *)&d_sink, (void *)&xw, (void *)&tile};
+    return herr(hipLaunchKernel(fn, dim3(grid), dim3(kThreads), args, 0, (hipStream_t)stream));
 }
 
 int priskv_crc_ctx_create(int device, priskv_crc_ctx **out)
@@ -1607,6 +1639,28 @@ void priskv_crc_ctx_destroy(priskv_crc_ctx *c)
 
 int priskv_crc_ctx_device(const priskv_crc_ctx *ctx) { return ctx ? ctx->device : -EINVAL; }
 
+int priskv_crc_stream_release(const priskv_crc_ctx *ctx, void *stream)
+{
+    if (!ctx)
+        return -EINVAL;
+    DevGuard g(ctx->device);
+    if (!g.ok)
+        return -ENODEV;
+    const hipStream_t s = (hipStream_t)stream;
+    if (int rc = herr(hipStreamSynchronize(s))) // the slots' last uses
+        return rc;
+    const pthread_t self = pthread_self();
+    pthread_mutex_lock(&ctx->pool_lock);
+    for (priskv_crc_pool_slot *slots : {ctx->pool, ctx->cnt_pool})
+        for (int i = 0; i < NPOOL; i++) {
+            priskv_crc_pool_slot &q = slots[i];
+            if (!q.busy && q.homed && q.home == s && (s != hipStreamPerThread || pthread_equal(q.tid, self)))
+                q.homed = 0;
+        }
+    pthread_mutex_unlock(&ctx->pool_lock);
+    return 0;
+}
+
 int priskv_crc32_blocks_dev(const priskv_crc_ctx *ctx, const void *d_base, uint64_t nblocks,
                             uint32_t block_size, uint32_t *d_out, void *stream)
 {
@@ -1658,8 +1712,7 @@ int priskv_crc32_verify_dev(const priskv_crc_ctx *ctx, const void *d_base, const
         return -ENODEV;
     hipStream_t s = (hipStream_t)stream;
     // status first: a zero-length verify still reports {0, UINT64_MAX}
-    hipLaunchKernelGGL(crc_status_init_kernel, dim3(1), dim3(64), 0, s, (unsigned long long *)d_status);
-    if (int rc = herr(hipGetLastError()))
+    if (int rc = launch_k(crc_status_init_kernel, dim3(1), dim3(64), s, (unsigned long long *)d_status))
         return rc;
     if (n == 0)
         return 0;
@@ -1671,9 +1724,7 @@ int priskv_crc32_verify_dev(const priskv_crc_ctx *ctx, const void *d_base, const
     if (!rc) {
         const uint64_t want = (n + 255) / 256;
         const uint32_t grid = (uint32_t)(want < (uint64_t)ctx->num_cus * 4 ? want : (uint64_t)ctx->num_cus * 4);
-        hipLaunchKernelGGL(crc_verify_kernel, dim3(grid), dim3(256), 0, s, got, d_expected, n,
-                           (unsigned long long *)d_status);
-        rc = herr(hipGetLastError());
+        rc = launch_k(crc_verify_kernel, dim3(grid), dim3(256), s, got, d_expected, n, (unsigned long long *)d_status);
     }
     const int frc = sc.release();
     return rc ? rc : frc;
@@ -1694,9 +1745,8 @@ int priskv_crc_fill_splitmix_dev(const priskv_crc_ctx *ctx, void *d_dst, uint64_
     uint64_t want = (nbytes / 16 + 255) / 256;
     uint64_t cap = (uint64_t)ctx->num_cus * 16;
     uint32_t grid = (uint32_t)(want < cap ? (want ? want : 1) : cap);
-    hipLaunchKernelGGL(fill_splitmix_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, (uint8_t *)d_dst,
-                       nbytes, seed, word_offset);
-    return herr(hipGetLastError());
+    return launch_k(fill_splitmix_kernel, dim3(grid), dim3(256), (hipStream_t)stream, (uint8_t *)d_dst, nbytes, seed,
+                    word_offset);
 }
 
 int priskv_crc_host_register(void *h_base, uint64_t len)

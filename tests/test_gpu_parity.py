@@ -410,39 +410,45 @@ def test_few_large_extents(torch_cuda, ctx, ctx_noseg, lens):
 
 def test_read_roof_dev(torch_cuda, ctx):
     """priskv_crc_read_roof_dev (diagnostic read roof of the CRC kernel's
-    access pattern): runs for the plans bench.py measures (4 KiB, 64 KiB,
-    1 MiB incl. the split mode, few large blocks), XORs each wave's XOR of
-    its words into the zeroed sink -- the XOR of the sink equals the XOR of
-    the whole region's 32-bit words -- and refuses what it cannot mirror
-    (block sizes not multiples of 4 KiB, unaligned bases)."""
+    access pattern): every variant (the plan's own depth and occupancy, and
+    2 / 3 / 4 chunks in flight at one or two workgroups per CU) runs for the
+    plans bench.py measures (4 KiB, 64 KiB, 1 MiB incl. the split mode, few
+    large blocks); each launched wave stores the XOR of its words in its own
+    sink slot, so the XOR of the zeroed sink equals the XOR of the whole
+    region's 32-bit words; it refuses what it cannot mirror (block sizes not
+    multiples of 4 KiB, unaligned bases, unknown variants)."""
     import errno
+    from priskv_amd.crc import ROOF_SINK_WORDS, ROOF_VARIANTS
     torch = torch_cuda
     t = _region(torch, ctx, 256 << 20, SEED ^ 0x2F, 17)
     words = t[:256 << 20].view(torch.int32)
     want = int(np.bitwise_xor.reduce(words.cpu().numpy().view(np.uint32)))
+    sink = torch.zeros(ROOF_SINK_WORDS, dtype=torch.int32, device="cuda")
     for bs in (4096, 65536, 1 << 20, 64 << 20, 256 << 20):
         nb = (256 << 20) // bs
-        sink = torch.zeros(nb, dtype=torch.int32, device="cuda")
-        ctx.read_roof_dev(t, bs, sink, nblocks=nb)
-        torch.cuda.synchronize()
-        got = int(np.bitwise_xor.reduce(sink.cpu().numpy().view(np.uint32)))
-        assert got == want, (bs, hex(got), hex(want))
+        for v in range(ROOF_VARIANTS):
+            sink.zero_()
+            ctx.read_roof_dev(t, bs, sink, nblocks=nb, variant=v)
+            torch.cuda.synchronize()
+            got = int(np.bitwise_xor.reduce(sink.cpu().numpy().view(np.uint32)))
+            assert got == want, (bs, v, hex(got), hex(want))
     tiles = _ctx_env(PRISKV_CRC_TILE_MIN_GIB="0")  # the block-cyclic tile order at any size
     try:
         for bs in (4096, 65536):
             nb = (256 << 20) // bs
-            sink = torch.zeros(nb, dtype=torch.int32, device="cuda")
+            sink.zero_()
             tiles.read_roof_dev(t, bs, sink, nblocks=nb)
             torch.cuda.synchronize()
             got = int(np.bitwise_xor.reduce(sink.cpu().numpy().view(np.uint32)))
             assert got == want, ("tiles", bs, hex(got), hex(want))
     finally:
         tiles.close()
-    sink = torch.zeros(16, dtype=torch.int32, device="cuda")
-    for bs, off in ((1024, 0), (4100, 0), (4096, 4)):
-        with pytest.raises(OSError) as e:
-            ctx.read_roof_dev(t[off:], bs, sink, nblocks=4)
-        assert e.value.errno == errno.EINVAL
+    from priskv_amd.crc import lib
+    for bs, off, v in ((1024, 0, 0), (4100, 0, 0), (4096, 4, 0), (4096, 0, ROOF_VARIANTS)):
+        assert lib().priskv_crc_read_roof_dev(ctx.handle, t[off:].data_ptr(), 4, bs, v, sink.data_ptr(),
+                                              None) == -errno.EINVAL
+    with pytest.raises(ValueError):
+        ctx.read_roof_dev(t, 4096, sink[:16], nblocks=4)
 
 
 def test_verify_dev(torch_cuda, ctx):

@@ -204,6 +204,7 @@ def test_batch_entry_points_reject_bad_args_without_gpu():
     assert L.priskv_crc_batch_flush(None) == -22
     L.priskv_crc_batch_destroy(None)  # no-op
     assert L.priskv_crc32_blocks_host(None, 1, 1, 4096, 1) == -22
+    assert L.priskv_crc_stream_release(None, None) == -22
     assert L.priskv_crc_fill_splitmix_dev(None, 16, 16, 0, 0, None) == -22
     assert L.priskv_crc32_blocks_path(None, 1, 4096) == -22
     assert L.priskv_crc32_blocks_path(16, 1, 0) == -22

@@ -2,8 +2,8 @@
 // with plain hipMalloc'd memory and no torch in the process (tools only):
 // separates "the kernel" from "bench.py's process" when their numbers differ.
 // Usage: lib_timing [block_size] [nblocks] [launches] [rounds]
-// LIB_TIMING_ROOF=1: time priskv_crc_read_roof_dev (the plan's loads, no
-// hashing) instead; LIB_TIMING_RAMP=N: N ramp launches (default 400; fewer
+// LIB_TIMING_ROOF=v+1: time priskv_crc_read_roof_dev variant v (the plan's
+// loads, no hashing) instead; LIB_TIMING_RAMP=N: N ramp launches (default 400; fewer
 // under rocprofv3 --pmc, which serialises every dispatch).
 #include <hip/hip_runtime.h>
 
@@ -47,10 +47,13 @@ int main(int argc, char **argv)
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
-    const bool roof = getenv("LIB_TIMING_ROOF") && atoi(getenv("LIB_TIMING_ROOF"));
+    const int roof = getenv("LIB_TIMING_ROOF") ? atoi(getenv("LIB_TIMING_ROOF")) : 0;
+    uint32_t *sink = nullptr;
+    CK(hipMalloc((void **)&sink, PRISKV_CRC_ROOF_SINK_WORDS * 4));
     const int ramp = getenv("LIB_TIMING_RAMP") ? atoi(getenv("LIB_TIMING_RAMP")) : 400;
     auto call = [&]() {
-        return roof ? priskv_crc_read_roof_dev(ctx, d, nb, bs, o, s) : priskv_crc32_blocks_dev(ctx, d, nb, bs, o, s);
+        return roof ? priskv_crc_read_roof_dev(ctx, d, nb, bs, (uint32_t)(roof - 1), sink, s)
+                    : priskv_crc32_blocks_dev(ctx, d, nb, bs, o, s);
     };
     for (int i = 0; i < ramp; i++) // ramp
         call();
@@ -71,7 +74,7 @@ int main(int argc, char **argv)
     const double alg = (double)nb * (bs + 4);
     printf("{\"tool\": \"lib_timing\", \"roof\": %d, \"block_size\": %u, \"nblocks\": %llu, \"plan\": \"%s\", \"launches\": %d, "
            "\"median_ms\": %.4f, \"min_ms\": %.4f, \"max_ms\": %.4f, \"TBps_median\": %.3f}\n",
-           (int)roof, bs, (unsigned long long)nb, plan, k, ms[ms.size() / 2], ms[0], ms.back(), alg / ms[ms.size() / 2] / 1e9);
+           roof, bs, (unsigned long long)nb, plan, k, ms[ms.size() / 2], ms[0], ms.back(), alg / ms[ms.size() / 2] / 1e9);
     priskv_crc_ctx_destroy(ctx);
     return 0;
 }
