@@ -29,6 +29,12 @@
  *
  * Streams are passed as `void *` holding a hipStream_t (NULL = the legacy
  * default stream), so this header does not require the HIP headers.
+ *
+ * Stream capture: the *_dev calls may be captured into HIP graphs.  A
+ * captured call that needs scratch gets a device buffer owned by the graph
+ * being captured (freed after the graph and its instantiations are
+ * destroyed), so launches of one graph exec are safe back to back; two
+ * instantiations of the same captured graph must not run concurrently.
  */
 #ifndef PRISKV_CRC_GPU_H
 #define PRISKV_CRC_GPU_H

@@ -37,6 +37,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <new>
 #include <tuple>
 #include <type_traits>
 #include <vector>
@@ -186,13 +187,112 @@ inline int herr(hipError_t e)
 // call's kernel (1 x 256 MiB 54.7 -> 49.9 us per call without it; also with
 // the event carried by the kernel launch itself, hipExtLaunchKernel, 4.6 us:
 // profiles/r04/pool_event/).  With no free slot of the stream's own or
-// unowned (more concurrent streams than slots), while the stream is
-// capturing, or with the pool off, it is a per-call hipMallocAsync /
-// hipFreeAsync, so a captured graph owns its own.
+// unowned (more concurrent streams than slots), or with the pool off, it is
+// a per-call hipMallocAsync / hipFreeAsync.
+//
+// While the stream is capturing, the scratch is a plain device allocation
+// the captured graph owns (graph_scratch): graph memory nodes (hipMallocAsync
+// inside a capture) returned wrong CRCs in round 5 -- the first three
+// back-to-back launches of a freshly captured graph, after other graphs of
+// the process had been destroyed, left 6-16 of 1900 split-mode blocks wrong
+// in most processes, and the same graph with dedicated memory did not
+// (tools/graph_race_probe.py).
 //
 // zero: the memory must read as zeros when a call gets it.  Then `slots` is a
 // pool whose users leave their slot zeroed (the fused extents kernel's
 // counters): a new allocation is cleared once, a reused slot is not.
+constexpr int kGraphOwned = -2; // Scratch::slot of a captured call's graph-owned allocation
+
+// Scratch of a call captured into a graph: a hipMalloc'd buffer (allocated in
+// relaxed capture mode, so a global-mode capture is not invalidated) tied to
+// the graph being captured by a user object, whose destructor runs when the
+// graph and every instantiation of it are gone.  Destructors must not call
+// HIP, so it queues the buffer; priskv_crc calls outside capture (and
+// ctx_destroy) free the queue.  One buffer per captured call: launches of one
+// graph exec are ordered, so only two instantiations of one graph launched
+// concurrently could share it (documented in the header).
+struct DeferredFree {
+    void *p;
+    int device;
+};
+pthread_mutex_t g_defer_lock = PTHREAD_MUTEX_INITIALIZER;
+std::vector<DeferredFree> g_deferred;
+volatile int g_deferred_n = 0;
+
+void graph_scratch_release(void *arg)
+{
+    DeferredFree *d = static_cast<DeferredFree *>(arg);
+    pthread_mutex_lock(&g_defer_lock);
+    try {
+        g_deferred.push_back(*d);
+        g_deferred_n = (int)g_deferred.size();
+    } catch (...) { // out of host memory: leak the buffer rather than call HIP here
+    }
+    pthread_mutex_unlock(&g_defer_lock);
+    delete d;
+}
+
+// free the buffers of destroyed graphs (outside capture: hipFree
+// synchronises; relaxed mode, so another thread's global-mode capture does
+// not make it an error)
+void free_deferred()
+{
+    if (!g_deferred_n)
+        return;
+    hipStreamCaptureMode mode = hipStreamCaptureModeRelaxed;
+    (void)hipThreadExchangeStreamCaptureMode(&mode);
+    std::vector<DeferredFree> todo;
+    pthread_mutex_lock(&g_defer_lock);
+    todo.swap(g_deferred);
+    g_deferred_n = 0;
+    pthread_mutex_unlock(&g_defer_lock);
+    int old = -1;
+    (void)hipGetDevice(&old);
+    for (const DeferredFree &d : todo) {
+        (void)hipSetDevice(d.device);
+        (void)hipFree(d.p);
+    }
+    if (old >= 0)
+        (void)hipSetDevice(old);
+    (void)hipThreadExchangeStreamCaptureMode(&mode);
+}
+
+int graph_scratch(const priskv_crc_ctx *ctx, hipStream_t s, size_t bytes, void **out)
+{
+    hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+    unsigned long long id = 0;
+    hipGraph_t graph = nullptr;
+    const hipGraphNode_t *deps = nullptr;
+    size_t ndeps = 0;
+    if (hipStreamGetCaptureInfo_v2(s, &st, &id, &graph, &deps, &ndeps) != hipSuccess ||
+        st != hipStreamCaptureStatusActive || !graph)
+        return -EIO;
+    hipStreamCaptureMode mode = hipStreamCaptureModeRelaxed;
+    if (hipThreadExchangeStreamCaptureMode(&mode) != hipSuccess)
+        return -EIO;
+    void *p = nullptr;
+    int rc = herr(hipMalloc(&p, bytes ? bytes : 4));
+    (void)hipThreadExchangeStreamCaptureMode(&mode);
+    if (rc)
+        return rc;
+    DeferredFree *d = new (std::nothrow) DeferredFree{p, ctx->device};
+    hipUserObject_t obj = nullptr;
+    if (!d || hipUserObjectCreate(&obj, d, graph_scratch_release, 1, hipUserObjectNoDestructorSync) != hipSuccess) {
+        delete d;
+        mode = hipStreamCaptureModeRelaxed;
+        (void)hipThreadExchangeStreamCaptureMode(&mode);
+        (void)hipFree(p);
+        (void)hipThreadExchangeStreamCaptureMode(&mode);
+        return -ENOMEM;
+    }
+    if (hipGraphRetainUserObject(graph, obj, 1, hipGraphUserObjectMove) != hipSuccess) {
+        (void)hipUserObjectRelease(obj, 1); // runs the destructor: the buffer goes to the deferred queue
+        return -EIO;
+    }
+    *out = p;
+    return 0;
+}
+
 struct Scratch {
     const priskv_crc_ctx *ctx;
     hipStream_t s;
@@ -214,7 +314,16 @@ struct Scratch {
     int get(size_t bytes)
     {
         hipStreamCaptureStatus cs = hipStreamCaptureStatusActive;
-        if (ctx->pool_ready && hipStreamIsCapturing(s, &cs) == hipSuccess && cs == hipStreamCaptureStatusNone) {
+        const bool capt_ok = hipStreamIsCapturing(s, &cs) == hipSuccess;
+        if (capt_ok && cs == hipStreamCaptureStatusActive) {
+            if (int rc = graph_scratch(ctx, s, bytes, &p))
+                return rc;
+            slot = kGraphOwned;
+            return zero ? zero_fill(p, bytes) : 0; // a kernel node: every replay starts from zeros
+        }
+        if (capt_ok && cs == hipStreamCaptureStatusNone)
+            free_deferred();
+        if (ctx->pool_ready && capt_ok && cs == hipStreamCaptureStatusNone) {
             // hipStreamPerThread is one handle that names a different stream
             // on every host thread: its slots belong to (handle, thread)
             const bool pt = s == hipStreamPerThread;
@@ -292,6 +401,8 @@ struct Scratch {
     // after the call's work is enqueued on s
     int release()
     {
+        if (slot == kGraphOwned) // the captured graph frees it
+            return 0;
         if (slot < 0)
             return p ? herr(hipFreeAsync(p, s)) : 0;
         priskv_crc_pool_slot &q = slots[slot];
@@ -508,6 +619,7 @@ int plan_for(uint32_t bs, uint64_t nblocks = 0)
 }
 
 constexpr int prio_free(int opt) { return opt & ~(3 << 8); }
+constexpr int plan_waves(int p) { return (kPlans[p].opt & 1024) ? 16 : kWaves; } // waves per workgroup
 
 template <int G, int CH, int NB, int OPT>
 const void *plan_kernel()
@@ -594,6 +706,7 @@ int launch_plan(const priskv_crc_ctx *ctx, int p, const uint8_t *base, uint64_t 
     const Plan &P = kPlans[p];
     const int gi = P.G == 64 ? 0 : (P.G == 32 ? 1 : 2);
     const uint64_t max_wgs = (uint64_t)ctx->num_cus * ctx->plan_wgs_per_cu[p];
+    const uint64_t NW = (uint64_t)plan_waves(p);
     const uint64_t nb_per_group = 64 / P.G;
     const uint64_t cps = bs / ((uint64_t)P.CH * 16u * P.G);
     const uint32_t *img = ctx->d_lds_image[gi];
@@ -601,31 +714,31 @@ int launch_plan(const priskv_crc_ctx *ctx, int p, const uint8_t *base, uint64_t 
     const uint32_t *zp = ctx->d_zpow;
     if (split > 1) { // one launch over ngroups * split units (host-checked: < 2^31 chunks per wave)
         uint64_t n = ngroups * split;
-        const uint64_t want = (n + kWaves - 1) / kWaves;
+        const uint64_t want = (n + NW - 1) / NW;
         const uint32_t grid = (uint32_t)(want < max_wgs ? want : max_wgs);
         uint32_t xw = split_units_xw(ctx, p, n), tile = 0;
         void *args[] = {(void *)&base, (void *)&n,    (void *)&bs,    (void *)&img,   (void *)&fold,
                         (void *)&out,  (void *)&xw,   (void *)&tile,  (void *)&stride, (void *)&split,
                         (void *)&zp,   (void *)&cnt,  (void *)&xacc};
-        return herr(hipLaunchKernel(plan_fn(p, ctx->prio, true), dim3(grid), dim3(kThreads), args, 0, s));
+        return herr(hipLaunchKernel(plan_fn(p, ctx->prio, true), dim3(grid), dim3(64 * NW), args, 0, s));
     }
     // the kernel counts a wave's chunks in 32 bits: cap groups per launch
-    const uint64_t cap = max_wgs * kWaves * ((1ull << 31) / cps - 1);
+    const uint64_t cap = max_wgs * NW * ((1ull << 31) / cps - 1);
     for (uint64_t done = 0; done < ngroups;) {
         uint64_t n = (ngroups - done < cap) ? ngroups - done : cap;
-        const uint64_t want = (n + kWaves - 1) / kWaves;
+        const uint64_t want = (n + NW - 1) / NW;
         const uint32_t grid = (uint32_t)(want < max_wgs ? want : max_wgs);
         const uint8_t *b = base + done * nb_per_group * stride;
         uint32_t *o = out + done * nb_per_group;
         // weights move whole groups: only worth it with many groups per wave
-        uint32_t xw = n >= 32ull * grid * kWaves ? ctx->plan_xw[p] : 0u;
+        uint32_t xw = n >= 32ull * grid * NW ? ctx->plan_xw[p] : 0u;
         uint32_t tile = tile_groups(ctx, n, nb_per_group * stride);
         uint32_t one = 1;
         uint32_t *none = nullptr;
         void *args[] = {(void *)&b,  (void *)&n,    (void *)&bs,   (void *)&img,    (void *)&fold,
                         (void *)&o,  (void *)&xw,   (void *)&tile, (void *)&stride, (void *)&one,
                         (void *)&zp, (void *)&none, (void *)&none};
-        if (int rc = herr(hipLaunchKernel(plan_fn(p, ctx->prio), dim3(grid), dim3(kThreads), args, 0, s)))
+        if (int rc = herr(hipLaunchKernel(plan_fn(p, ctx->prio), dim3(grid), dim3(64 * NW), args, 0, s)))
             return rc;
         done += n;
     }
@@ -1291,7 +1404,7 @@ int rows_occupancy(priskv_crc_ctx *c)
 {
     for (int p = 0; p < NPLANS; p++) {
         int n = 0;
-        hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, plan_fn(p, c->prio), kThreads, 0);
+        hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, plan_fn(p, c->prio), 64 * plan_waves(p), 0);
         if (e != hipSuccess)
             return herr(e);
         c->plan_wgs_per_cu[p] = n < 1 ? 1 : (n < kPlans[p].wg_per_cu ? n : kPlans[p].wg_per_cu);
@@ -1592,6 +1705,7 @@ void priskv_crc_ctx_destroy(priskv_crc_ctx *c)
     if (!c)
         return;
     DevGuard g(c->device);
+    free_deferred();
     if (c->stream_ready) {
         for (int i = 0; i < NSTREAM; i++) {
             (void)hipStreamSynchronize(c->streams[i]);
