@@ -78,7 +78,7 @@ struct priskv_crc_ctx {
     int balance;               // byte-balanced extents split (PRISKV_CRC_BALANCE=0: off)
     int head_split;            // rows kernel + head terms for B = h + whole KiB rows (PRISKV_CRC_HEADSPLIT=0: off)
     uint64_t seg_max_extents;  // device-resident lengths: segment calls of at most this many extents
-    int xcd_rr;                // the XCD probe found workgroup b on XCD b % 8 (weights apply)
+    int xcd_rr;                // the XCD probe found round-robin dispatch: workgroup b on XCD (b + k) % 8 (weights apply)
     uint64_t tile_min_bytes;   // rows batches of at least this many bytes run in block-cyclic tiles
     uint64_t tile_bytes;       // ... of about this many bytes each
     uint32_t *d_lds_image[3];  // 64 KiB each: set B gap for G = 64, 32, 16
@@ -1350,7 +1350,7 @@ int launch_blocks(const priskv_crc_ctx *ctx, const uint8_t *base, uint64_t nbloc
 // (workgroups dispatched round-robin over 8 XCDs) waves on odd XCDs finish
 // later under an equal split on every MI355X measured, so even-XCD waves take
 // more parts (kPlans[p].we : wo).  Only when the context's probe saw
-// workgroup b on XCD b % 8 (xcd_rr); otherwise -- another partition mode, a
+// workgroup b on XCD (b + k) % 8 (xcd_rr); otherwise -- another partition mode, a
 // different XCD count -- the split is equal.  PRISKV_CRC_XCD_WEIGHTS="we:wo"
 // overrides every plan ("1:1" = equal split) and applies regardless.
 uint32_t xcd_weights(int xcd_rr, int p)
@@ -1368,7 +1368,8 @@ uint32_t xcd_weights(int xcd_rr, int p)
     return we == wo ? 0u : ((we << 16) | wo);
 }
 
-// Does workgroup b of a launch run on XCD b % 8 (8 XCDs, round-robin)?
+// Does workgroup b of a launch run on XCD (b + k) % 8 (8 XCDs, round-robin
+// from some first XCD k)?
 // One launch of 64 single-wave workgroups on the context's stream.
 // PRISKV_CRC_XCD_PROBE=0 forces "no" (tests of the fallback).
 int xcd_probe(priskv_crc_ctx *c, int *rr)
@@ -1391,9 +1392,11 @@ int xcd_probe(priskv_crc_ctx *c, int *rr)
     (void)hipFree(d);
     if (rc)
         return rc;
-    int ok = 1;
+    // round-robin from the queue's first XCD (which differs by hardware queue:
+    // the kernels read its parity themselves, wave_range)
+    int ok = h[0] < 8;
     for (int b = 0; b < kProbeWgs; b++)
-        ok &= h[b] == (uint32_t)(b % 8);
+        ok &= h[b] == (h[0] + (uint32_t)b) % 8;
     *rr = ok;
     return 0;
 }
