@@ -22,6 +22,9 @@ import torch
 ARGS = [a for a in sys.argv[1:] if not a.startswith("--")]
 ROUNDS = int(next((a.split("=", 1)[1] for a in sys.argv if a.startswith("--rounds=")), "3"))
 ONLY = next((a.split("=", 1)[1].split("+") for a in sys.argv if a.startswith("--cases=")), None)
+# --streams=K: time every case on each of K created streams (HIP maps streams to
+# hardware queues, whose first XCD differs: round 5), tagging lines with "stream"
+NSTREAMS = int(next((a.split("=", 1)[1] for a in sys.argv if a.startswith("--streams=")), "1"))
 C = ctypes
 
 
@@ -44,7 +47,8 @@ def load(spec):
 
 libs = {a: load(a) for a in ARGS}
 TAGS = list(libs)
-s = torch.cuda.Stream()
+STREAMS = [torch.cuda.Stream() for _ in range(NSTREAMS)]
+s = STREAMS[0]
 region = torch.empty(4 << 30, dtype=torch.uint8, device="cuda")
 g = torch.Generator(device="cuda").manual_seed(7)
 region.random_(0, 256, generator=g)
@@ -95,8 +99,9 @@ for r in range(ROUNDS):
             continue
         k = (r + ci) % len(TAGS)
         order = TAGS[k:] + TAGS[:k]
-        for tag in order:
+        for si, tag in [(si, tag) for si in range(NSTREAMS) for tag in order]:
             L, h = libs[tag]
+            s = STREAMS[si]
             sp = s.cuda_stream
 
             def call():
@@ -117,5 +122,7 @@ for r in range(ROUNDS):
             got = out.cpu().numpy().tobytes()
             if "--nocheck" not in sys.argv:  # (--nocheck: timing-only probes of deliberately wrong builds)
                 assert ref.setdefault(name, got) == got, (name, tag)  # A and B agree bit for bit
-            print(json.dumps({"round": r, "case": name, "variant": tag, "us_per_call": round(e0.elapsed_time(e1) / 50 * 1e3, 2)}),
-                  flush=True)
+            rec = {"round": r, "case": name, "variant": tag, "us_per_call": round(e0.elapsed_time(e1) / 50 * 1e3, 2)}
+            if NSTREAMS > 1:
+                rec["stream"] = si
+            print(json.dumps(rec), flush=True)
