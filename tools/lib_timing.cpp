@@ -50,7 +50,10 @@ int main(int argc, char **argv)
     const int roof = getenv("LIB_TIMING_ROOF") ? atoi(getenv("LIB_TIMING_ROOF")) : 0;
     uint32_t *sink = nullptr;
     CK(hipMalloc((void **)&sink, PRISKV_CRC_ROOF_SINK_WORDS * 4));
-    const int ramp = getenv("LIB_TIMING_RAMP") ? atoi(getenv("LIB_TIMING_RAMP")) : 400;
+    // default ramp: 400 launches up to 4 GiB per call, ~1.6 TiB of reads above
+    const uint64_t nbytes = (uint64_t)bs * nb;
+    const int ramp_default = nbytes <= (4ull << 30) ? 400 : (int)std::max<uint64_t>(20, (400ull << 32) / nbytes);
+    const int ramp = getenv("LIB_TIMING_RAMP") ? atoi(getenv("LIB_TIMING_RAMP")) : ramp_default;
     auto call = [&]() {
         return roof ? priskv_crc_read_roof_dev(ctx, d, nb, bs, (uint32_t)(roof - 1), sink, s)
                     : priskv_crc32_blocks_dev(ctx, d, nb, bs, o, s);
