@@ -97,6 +97,11 @@ for r in range(ROUNDS):
         out = torch.empty(n, dtype=torch.int32, device="cuda")
         if ONLY and not any(o in name for o in ONLY):
             continue
+        # offs / lens are written on torch's current stream; the calls run on
+        # STREAMS[si]: wait for them (round 5: without this a call read the
+        # arrays of a reused allocation before they were written -- garbage
+        # offsets, an illegal-address fault in the tool)
+        torch.cuda.synchronize()
         k = (r + ci) % len(TAGS)
         order = TAGS[k:] + TAGS[:k]
         for si, tag in [(si, tag) for si in range(NSTREAMS) for tag in order]:
