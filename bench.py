@@ -251,7 +251,8 @@ def read_roof(B, region, bs, nb, stream, alg, k):
             "measured_peak_source": "priskv_crc_read_roof_dev on the same region in this process: the CRC kernel's "
                                     "loads, per-wave ranges and XCD split without hashing, best of "
                                     f"{ROOF_VARIANTS} variants (variant 0 = the CRC plan's own pipeline depth and "
-                                    "occupancy; 1-6 = 2/2/3/3/4/4 chunks in flight at 1/2 workgroups per CU); "
+                                    "occupancy; 1-6 = 2/2/3/3/4/4 chunks in flight at 1/2 workgroups per CU; 7-8 = "
+                                    "the plan's shape with progress priority 1/3); "
                                     f"mean of {k} launches each (one event pair per launch) after a ramp",
             "roof_launch_ms": st}
 

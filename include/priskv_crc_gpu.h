@@ -224,16 +224,17 @@ int priskv_crc32_blocks_plan(const priskv_crc_ctx *ctx, const void *d_base, uint
  * XCD split crc_rows_kernel uses for this block size (block_size a multiple
  * of 4 KiB, d_base 16-byte aligned), without hashing.  variant 0 runs in the
  * CRC plan's own pipeline depth and occupancy; variants 1 ..
- * PRISKV_CRC_ROOF_VARIANTS - 1 in 2, 2, 3, 3, 4, 4 chunks in flight at one /
- * two 8-wave workgroups per CU, so the best variant bounds what HBM gives
- * this pattern.  d_sink: PRISKV_CRC_ROOF_SINK_WORDS uint32 entries; launched
+ * 6 in 2, 2, 3, 3, 4, 4 chunks in flight at one / two 8-wave workgroups per
+ * CU, variants 7 and 8 in the plan's shape with the CRC kernels' progress
+ * priority (modes 1 / 3), so the best variant bounds what HBM gives this
+ * pattern.  d_sink: PRISKV_CRC_ROOF_SINK_WORDS uint32 entries; launched
  * wave w stores the XOR of the 32-bit words it read in d_sink[w] (plain
  * stores, other entries untouched), so over a zeroed sink the XOR of all
  * entries is the XOR of the batch's words.  Timing it beside
  * priskv_crc32_blocks_dev on the same region gives the fraction of this
  * pattern's roof the CRC reaches.  Asynchronous on stream; 0, or -EINVAL
  * (also for a batch of more than 2^31 chunks per wave) / -ENODEV / -EIO. */
-#define PRISKV_CRC_ROOF_VARIANTS 7
+#define PRISKV_CRC_ROOF_VARIANTS 9
 #define PRISKV_CRC_ROOF_SINK_WORDS 8192
 int priskv_crc_read_roof_dev(const priskv_crc_ctx *ctx, const void *d_base, uint64_t nblocks,
                              uint32_t block_size, uint32_t variant, uint32_t *d_sink, void *stream);

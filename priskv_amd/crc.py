@@ -32,7 +32,7 @@ PATH_NAMES = {PATH_ROWS: "rows", PATH_EXTENTS: "extents", PATH_SMALL: "small", P
 _lib: Optional[ctypes.CDLL] = None
 
 # include/priskv_crc_gpu.h: read-roof variants and sink size
-ROOF_VARIANTS = 7
+ROOF_VARIANTS = 9
 ROOF_SINK_WORDS = 8192
 
 # (name, restype, argtypes) for every symbol the two headers declare

@@ -1539,8 +1539,10 @@ int priskv_crc_read_roof_dev(const priskv_crc_ctx *ctx, const void *d_base, uint
         S = split_for(ctx, nblocks, block_size);
     else if ((S = split_few(ctx, nblocks, block_size)) > 1)
         p = PLAN_SPLIT_DEEP;
-    const int nbuf = variant ? 2 + (int)(variant - 1) / 2 : kPlans[p].NBUF;
-    const uint64_t wgpc = variant ? 1 + (variant - 1) % 2 : (uint64_t)ctx->plan_wgs_per_cu[p];
+    // variants 7-8: the plan's shape with progress priority mode 1 / 3
+    const int nbuf = (variant && variant < 7) ? 2 + (int)(variant - 1) / 2 : kPlans[p].NBUF;
+    const uint64_t wgpc = (variant && variant < 7) ? 1 + (variant - 1) % 2 : (uint64_t)ctx->plan_wgs_per_cu[p];
+    const int prio = variant == 7 ? 1 : variant == 8 ? 3 : 0;
     const uint64_t max_wgs = (uint64_t)ctx->num_cus * wgpc;
     block_size /= S;
     nblocks *= S;
@@ -1556,9 +1558,15 @@ int priskv_crc_read_roof_dev(const priskv_crc_ctx *ctx, const void *d_base, uint
     uint32_t tile = S == 1 ? tile_groups(ctx, nblocks, bs) : 0u; // the CRC kernel's tiles (G = 64: a group is a block)
     if (tile)
         xw = 0;
-    const void *fn = nbuf == 4   ? reinterpret_cast<const void *>(&crc_read_roof_kernel<4, 4, kAux>)
-                     : nbuf == 3 ? reinterpret_cast<const void *>(&crc_read_roof_kernel<4, 3, kAux>)
-                                 : reinterpret_cast<const void *>(&crc_read_roof_kernel<4, 2, kAux>);
+    const void *fn = nbuf == 4   ? (prio == 1   ? reinterpret_cast<const void *>(&crc_read_roof_kernel<4, 4, kAux, 1>)
+                                    : prio == 3 ? reinterpret_cast<const void *>(&crc_read_roof_kernel<4, 4, kAux, 3>)
+                                                : reinterpret_cast<const void *>(&crc_read_roof_kernel<4, 4, kAux>))
+                     : nbuf == 3 ? (prio == 1   ? reinterpret_cast<const void *>(&crc_read_roof_kernel<4, 3, kAux, 1>)
+                                    : prio == 3 ? reinterpret_cast<const void *>(&crc_read_roof_kernel<4, 3, kAux, 3>)
+                                                : reinterpret_cast<const void *>(&crc_read_roof_kernel<4, 3, kAux>))
+                                 : (prio == 1   ? reinterpret_cast<const void *>(&crc_read_roof_kernel<4, 2, kAux, 1>)
+                                    : prio == 3 ? reinterpret_cast<const void *>(&crc_read_roof_kernel<4, 2, kAux, 3>)
+                                                : reinterpret_cast<const void *>(&crc_read_roof_kernel<4, 2, kAux>));
     void *args[] = {(void *)&b, (void *)&nblocks, (void *)&bs, (void *)&d_sink, (void *)&xw, (void *)&tile};
     return herr(hipLaunchKernel(fn, dim3(grid), dim3(kThreads), args, 0, (hipStream_t)stream));
 }
