@@ -52,10 +52,8 @@ typedef struct priskv_crc_ctx priskv_crc_ctx;
  * LDS images, nibble fold tables, shift matrices) and sizes the persistent
  * grid from the device's CU count.  *out is set only on success.
  * PRISKV_CRC_SEGMENT=0 in the environment at creation turns off the
- * segmentation of few large blocks / extents, PRISKV_CRC_PRIO=0 the
- * kernels' progress priority, PRISKV_CRC_BALANCE=0 the byte-balanced
- * extents split and PRISKV_CRC_STRIDE=0 the uniform-stride kernel
- * (measurement only). */
+ * segmentation of few large blocks / extents, PRISKV_CRC_BALANCE=0 the
+ * byte-balanced extents split (measurement only). */
 int priskv_crc_ctx_create(int device, priskv_crc_ctx **out);
 void priskv_crc_ctx_destroy(priskv_crc_ctx *ctx);
 int priskv_crc_ctx_device(const priskv_crc_ctx *ctx);
@@ -198,14 +196,13 @@ int priskv_crc_fill_splitmix_dev(const priskv_crc_ctx *ctx, void *d_dst, uint64_
  * blocks are hashed as segments and combined), 3 = sub-KiB power-of-two
  * blocks (16-byte aligned base), 5 = uniform stride (any other block of
  * 16 B up to 9 KiB: rows aligned to each block's end), 2 = extents (the
- * larger such blocks, and every block beyond 64 MiB), 4 = generic (blocks
+ * larger such blocks), 4 = generic (blocks
  * below 16 B: one thread per block), 6 = head split (a multiple of 4 that is
  * whole KiB rows plus a 4-64 B head, 4-byte aligned base: the rows kernel on
  * the bodies, then the heads' terms; not for a batch of few blocks with
  * bodies of 64 KiB and more, which the extents path segments -- judged for a
- * 256-CU device).  Context options (PRISKV_CRC_STRIDE=0,
- * PRISKV_CRC_STRIDE_MAX_KIB) move the 5 / 2 boundary; the exact kernels a
- * given context launches, few-block segmentation included, are reported by
+ * 256-CU device).  The exact kernels a given context launches, few-block
+ * segmentation included, are reported by
  * priskv_crc32_blocks_plan.  For tests and benchmarks; -EINVAL for invalid
  * arguments. */
 int priskv_crc32_blocks_path(const void *d_base, uint64_t nblocks, uint32_t block_size);
@@ -214,7 +211,7 @@ int priskv_crc32_blocks_path(const void *d_base, uint64_t nblocks, uint32_t bloc
  * this context, as a NUL-terminated description in buf (at most len bytes),
  * e.g. "crc_rows_kernel<G=64,CH=4,NBUF=3,nt,pipelined-fold,nibble-fold,
  * progress-priority 3,xcd-weighted 31:29>".  It reflects the context's
- * options (PRISKV_CRC_PRIO / _SEGMENT / _XCD_WEIGHTS and the XCD probe).
+ * options (PRISKV_CRC_SEGMENT / _SPLIT / _XCD_WEIGHTS and the XCD probe).
  * Benchmarks and diagnostics; -EINVAL for invalid arguments. */
 int priskv_crc32_blocks_plan(const priskv_crc_ctx *ctx, const void *d_base, uint64_t nblocks, uint32_t block_size,
                              char *buf, uint64_t len);

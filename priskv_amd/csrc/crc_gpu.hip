@@ -69,12 +69,10 @@ struct priskv_crc_pool_slot {
 struct priskv_crc_ctx {
     int device;
     int num_cus;
-    int max_wgs;               // resident workgroups of the sub-KiB kernel (2 per CU)
     int plan_wgs_per_cu[16];   // resident workgroups per CU of each rows-kernel plan
     uint32_t plan_xw[16];      // rows-kernel split per plan: (even << 16) | odd XCD weight, 0 = equal
     int segment;               // split few large blocks / extents into segments (PRISKV_CRC_SEGMENT=0: off)
     int split;                 // rows kernel split mode for few blocks per wave (PRISKV_CRC_SPLIT=0: off)
-    int prio;                  // rows kernel progress priority (PRISKV_CRC_PRIO=0: off)
     int balance;               // byte-balanced extents split (PRISKV_CRC_BALANCE=0: off)
     int head_split;            // rows kernel + head terms for B = h + whole KiB rows (PRISKV_CRC_HEADSPLIT=0: off)
     uint64_t seg_max_extents;  // device-resident lengths: segment calls of at most this many extents
@@ -86,8 +84,6 @@ struct priskv_crc_ctx {
     uint32_t *d_nibrep[7];     // nibble fold tables for G = 1 << j (j >= 1), 8 x 16 x max(G, 32) words
     uint32_t *d_nib16;         // the extents kernel's: G = 16, width 16 (8 KiB)
     uint32_t *d_small_img[5];  // sub-KiB byte-fold images for G = 1 << j, j = 1..4 (prv_small_image)
-    int small_bf;              // sub-KiB kernel folds through byte tables (PRISKV_CRC_SMALL_BF=0: nibble tables)
-    int stride_prio;           // stride kernel: progress-priority mode in one 16-wave workgroup per CU (0 with PRIO=0)
     uint32_t *d_sarwate;       // 256 words
     uint32_t *d_zpow;          // kZpowRows x 32 words: columns of Z_(2^k) (segment combine)
     uint32_t *d_rowshift;      // 16 x 4 x 32 words: columns of Z_-p o Z_(256(3-k)) (extents fold)
@@ -112,12 +108,6 @@ struct priskv_crc_ctx {
     // allocated; the kernel leaves the counters zero; guarded by pool_lock)
     mutable priskv_crc_pool_slot cnt_pool[NPOOL];
     int fused;                 // few extents in one launch (PRISKV_CRC_FUSED=0: the three-launch path)
-    int fused_xw;              // fused kernel: XCD-weighted split of finer segments (PRISKV_CRC_FUSED_XW=0: off)
-    int stride;                // odd block sizes / unaligned bases take crc_stride_kernel (PRISKV_CRC_STRIDE=0: the
-                               // extents / generic kernels, as in round 2)
-    int stride_g;              // PRISKV_CRC_STRIDE_G: force the stride kernel's G (0 = cost model; tests)
-    uint64_t stride_max;       // blocks from this size (multiples of 4) take the extents path,
-    uint64_t stride_odd_max;   // and odd ones from this (PRISKV_CRC_STRIDE_MAX_KIB sets both; tests)
 };
 
 namespace {
@@ -419,19 +409,15 @@ inline bool is_pow2(uint64_t v) { return v && !(v & (v - 1)); }
 
 enum Path { PATH_ROWS = 1, PATH_EXTENTS = 2, PATH_SMALL = 3, PATH_GENERIC = 4, PATH_STRIDE = 5, PATH_HEAD = 6 };
 
-// stride = 0: round 2's dispatch of odd sizes / unaligned bases (extents from
-// 1 KiB, generic below)
-int choose_path(const void *d_base, uint32_t block_size, int stride = 1)
+int choose_path(const void *d_base, uint32_t block_size)
 {
     const bool aligned = ((uintptr_t)d_base & 15) == 0;
     if (aligned && block_size % PRV_ROW_BYTES == 0)
         return PATH_ROWS;
     if (aligned && is_pow2(block_size) && block_size >= 16 && block_size <= 512)
         return PATH_SMALL;
-    if (stride && block_size >= 16)
+    if (block_size >= 16)
         return PATH_STRIDE;
-    if (block_size >= PRV_ROW_BYTES)
-        return PATH_EXTENTS;
     return PATH_GENERIC;
 }
 
@@ -486,7 +472,6 @@ int launch_ext_kernel(const priskv_crc_ctx *ctx, bool seg, bool many, bool bal, 
     void *args[] = {(void *)&abase, (void *)&n,   (void *)&offs, (void *)&lens,   (void *)&shift,
                     (void *)&stride, (void *)&len_const, (void *)&img, (void *)&nib, (void *)&rs,
                     (void *)&out,   (void *)&prefix, (void *)&shifts, (void *)&zpow, (void *)&sub};
-    many = many && ctx->prio;
     const int waves = many ? kExtWaves * kExtWgPerCu : kExtWaves;
     const uint64_t cap = (uint64_t)ctx->num_cus * (many ? 1 : kExtWgPerCu);
     // segmented: the grid covers every resident wave (the kernel reads the
@@ -618,7 +603,6 @@ int plan_for(uint32_t bs, uint64_t nblocks = 0)
     return R % 2 == 0 ? PLAN_G64_CH2 : PLAN_G64_CH1;
 }
 
-constexpr int prio_free(int opt) { return opt & ~(3 << 8); }
 constexpr int plan_waves(int p) { return (kPlans[p].opt & 1024) ? 16 : kWaves; } // waves per workgroup
 
 template <int G, int CH, int NB, int OPT>
@@ -627,41 +611,39 @@ const void *plan_kernel()
     return reinterpret_cast<const void *>(&crc_rows_kernel<G, CH, NB, kAux, OPT>);
 }
 
-// prio = false: the plan's kernel without progress priority (PRISKV_CRC_PRIO=0);
-// split: its split-mode instance (plans with one block per wave group and an
-// unpipelined fold: plan_splits)
+// split: the plan's split-mode instance (plans with one block per wave group
+// and an unpipelined fold: plan_splits)
 constexpr int kSplitOpt = 64, kMergeOpt = 128;
 constexpr bool plan_splits(int p) { return kPlans[p].G == 64 && !(kPlans[p].opt & 2); }
 
 template <int P>
-const void *plan_kernel_p(bool prio, bool split)
+const void *plan_kernel_p(bool split)
 {
     constexpr Plan Q = kPlans[P];
-    constexpr int O = prio_free(Q.opt);
     if constexpr (plan_splits(P)) {
         // the few-large-blocks plan merges its parts per workgroup (a lone
         // block has a part in every wave; per-wave atomics elsewhere: the
         // workgroup barrier cost 2 % on 4 Ki x 1 MiB, profiles/r04/split/)
         constexpr int SO = kSplitOpt | (P == PLAN_SPLIT_DEEP ? kMergeOpt : 0);
         if (split)
-            return prio ? plan_kernel<Q.G, Q.CH, Q.NBUF, Q.opt | SO>() : plan_kernel<Q.G, Q.CH, Q.NBUF, O | SO>();
+            return plan_kernel<Q.G, Q.CH, Q.NBUF, Q.opt | SO>();
     }
-    return prio ? plan_kernel<Q.G, Q.CH, Q.NBUF, Q.opt>() : plan_kernel<Q.G, Q.CH, Q.NBUF, O>();
+    return plan_kernel<Q.G, Q.CH, Q.NBUF, Q.opt>();
 }
 
-const void *plan_fn(int p, bool prio, bool split = false)
+const void *plan_fn(int p, bool split = false)
 {
     switch (p) {
-    case PLAN_4K: return plan_kernel_p<PLAN_4K>(prio, split);
-    case PLAN_G64_CH4_NIB: return plan_kernel_p<PLAN_G64_CH4_NIB>(prio, split);
-    case PLAN_G16_CH4_PIPE: return plan_kernel_p<PLAN_G16_CH4_PIPE>(prio, split);
-    case PLAN_G16_CH4: return plan_kernel_p<PLAN_G16_CH4>(prio, split);
-    case PLAN_G64_CH4: return plan_kernel_p<PLAN_G64_CH4>(prio, split);
-    case PLAN_G64_CH4_BIG: return plan_kernel_p<PLAN_G64_CH4_BIG>(prio, split);
-    case PLAN_G64_CH2: return plan_kernel_p<PLAN_G64_CH2>(prio, split);
-    case PLAN_SPLIT_DEEP: return plan_kernel_p<PLAN_SPLIT_DEEP>(prio, split);
-    case PLAN_4K_DEEP: return plan_kernel_p<PLAN_4K_DEEP>(prio, split);
-    default: return plan_kernel_p<PLAN_G64_CH1>(prio, split);
+    case PLAN_4K: return plan_kernel_p<PLAN_4K>(split);
+    case PLAN_G64_CH4_NIB: return plan_kernel_p<PLAN_G64_CH4_NIB>(split);
+    case PLAN_G16_CH4_PIPE: return plan_kernel_p<PLAN_G16_CH4_PIPE>(split);
+    case PLAN_G16_CH4: return plan_kernel_p<PLAN_G16_CH4>(split);
+    case PLAN_G64_CH4: return plan_kernel_p<PLAN_G64_CH4>(split);
+    case PLAN_G64_CH4_BIG: return plan_kernel_p<PLAN_G64_CH4_BIG>(split);
+    case PLAN_G64_CH2: return plan_kernel_p<PLAN_G64_CH2>(split);
+    case PLAN_SPLIT_DEEP: return plan_kernel_p<PLAN_SPLIT_DEEP>(split);
+    case PLAN_4K_DEEP: return plan_kernel_p<PLAN_4K_DEEP>(split);
+    default: return plan_kernel_p<PLAN_G64_CH1>(split);
     }
 }
 
@@ -720,7 +702,7 @@ int launch_plan(const priskv_crc_ctx *ctx, int p, const uint8_t *base, uint64_t 
         void *args[] = {(void *)&base, (void *)&n,    (void *)&bs,    (void *)&img,   (void *)&fold,
                         (void *)&out,  (void *)&xw,   (void *)&tile,  (void *)&stride, (void *)&split,
                         (void *)&zp,   (void *)&cnt,  (void *)&xacc};
-        return herr(hipLaunchKernel(plan_fn(p, ctx->prio, true), dim3(grid), dim3(64 * NW), args, 0, s));
+        return herr(hipLaunchKernel(plan_fn(p, true), dim3(grid), dim3(64 * NW), args, 0, s));
     }
     // the kernel counts a wave's chunks in 32 bits: cap groups per launch
     const uint64_t cap = max_wgs * NW * ((1ull << 31) / cps - 1);
@@ -738,7 +720,7 @@ int launch_plan(const priskv_crc_ctx *ctx, int p, const uint8_t *base, uint64_t 
         void *args[] = {(void *)&b,  (void *)&n,    (void *)&bs,   (void *)&img,    (void *)&fold,
                         (void *)&o,  (void *)&xw,   (void *)&tile, (void *)&stride, (void *)&one,
                         (void *)&zp, (void *)&none, (void *)&none};
-        if (int rc = herr(hipLaunchKernel(plan_fn(p, ctx->prio), dim3(grid), dim3(64 * NW), args, 0, s)))
+        if (int rc = herr(hipLaunchKernel(plan_fn(p), dim3(grid), dim3(64 * NW), args, 0, s)))
             return rc;
         done += n;
     }
@@ -920,10 +902,10 @@ int launch_fused(const priskv_crc_ctx *ctx, const uint8_t *base, uint64_t n, con
     const bool few = n <= kFusedFewExtents;
     const int nw = few ? 8 : kFusedWaves;
     const uint64_t waves = (uint64_t)ctx->num_cus * nw;
-    const uint64_t want = ctx->fused_xw ? kFusedUnitsPerWave * waves : seg_target(ctx);
+    const uint64_t want = kFusedUnitsPerWave * waves;
     const uint32_t tgt = 1u << (31 - __builtin_clz((uint32_t)std::min<uint64_t>(want, 1u << 30))); // a power of two
-    uint32_t ms = ctx->fused_xw ? kFusedMinShift : kSegMinShift;
-    uint32_t xw = ctx->fused_xw ? ctx->plan_xw[PLAN_4K] : 0u;
+    uint32_t ms = kFusedMinShift;
+    uint32_t xw = ctx->plan_xw[PLAN_4K];
     // (16 waves: 4- and 8-row chunks lost 6-13 % on a lone 256 MiB value, profiles/r03/fused/)
     // (8 waves: progress priority, 3-deep 4-row and 2-deep 8-row chunks all level, profiles/r04/fused/prio_depth_ab.jsonl)
     const void *fn =
@@ -1091,32 +1073,25 @@ constexpr int kSmallCh = 4, kSmallNbuf = 3, kSmallCh1 = 4, kSmallNbuf1 = 3;
 // byte-table fold (OPT bit 1) for G = 2..16: four lookups per fold instead
 // of eight nibble lookups (crc_device.inc byte_fold)
 template <int G>
-const void *small_fn_g(bool prio, bool bf)
+const void *small_fn_g()
 {
-    if constexpr (G <= 8) // without priority (two 8-wave workgroups per CU): the 64 KiB byte-fold image
-        if (bf && !prio)
-            return reinterpret_cast<const void *>(&crc_small_kernel<G, 3>);
-    if (bf && prio && G <= 16) // first chunks before the tables (OPT bit 2): 256 MiB calls -2.5-3 %, 4 GiB level
+    if constexpr (G <= 16) // first chunks before the tables (OPT bit 2): 256 MiB calls -2.5-3 %, 4 GiB level
         return reinterpret_cast<const void *>(&crc_small_kernel<G, kSmallOptPrio | 2 | 4, kSmallCh, kSmallNbuf>);
-    return prio ? reinterpret_cast<const void *>(&crc_small_kernel<G, kSmallOptPrio, kSmallCh, kSmallNbuf>)
-                : reinterpret_cast<const void *>(&crc_small_kernel<G, 1>);
+    return reinterpret_cast<const void *>(&crc_small_kernel<G, kSmallOptPrio, kSmallCh, kSmallNbuf>);
 }
 
-// byte fold for G = 2..8; for G = 16 only with progress priority: its 128 KiB
-// image leaves room for one workgroup per CU, which the 16-wave priority
-// shape fills and two 8-wave workgroups would not
-bool small_bf(const priskv_crc_ctx *ctx, int gl) { return ctx->small_bf && gl >= 1 && gl <= (ctx->prio ? 4 : 3); }
-
-const void *small_fn(int gl, bool prio, bool bf)
+// G = 1 << gl lanes per block: G = 2..16 fold through the byte tables, G = 32
+// through the nibble tables, G = 1 needs no fold; all in one 16-wave
+// workgroup per CU with progress priority
+const void *small_fn(int gl)
 {
     switch (gl) {
-    case 0: return prio ? reinterpret_cast<const void *>(&crc_small_kernel<1, kSmallOptPrio, kSmallCh1, kSmallNbuf1>)
-                        : reinterpret_cast<const void *>(&crc_small_kernel<1, 0, kSmallCh1, kSmallNbuf1>);
-    case 1: return small_fn_g<2>(prio, bf);
-    case 2: return small_fn_g<4>(prio, bf);
-    case 3: return small_fn_g<8>(prio, bf);
-    case 4: return small_fn_g<16>(prio, bf);
-    default: return small_fn_g<32>(prio, false);
+    case 0: return reinterpret_cast<const void *>(&crc_small_kernel<1, kSmallOptPrio, kSmallCh1, kSmallNbuf1>);
+    case 1: return small_fn_g<2>();
+    case 2: return small_fn_g<4>();
+    case 3: return small_fn_g<8>();
+    case 4: return small_fn_g<16>();
+    default: return small_fn_g<32>();
     }
 }
 
@@ -1133,36 +1108,21 @@ struct StridePlan {
     int G;
     uint32_t R;
 };
-constexpr uint32_t kStrideMaxBlock = 64u << 20; // larger odd blocks keep the (segmenting) extents path
-// Odd block sizes or bases (not multiples of 4) from 4.5 KiB, other sizes
-// from 9 KiB: the extents kernel's 16-B aligned windows and one fold per
-// block beat the stride kernel's per-row work once a block spans 9-10 of its
-// rows.  TB/s extents / stride, order-rotated, one process: odd 4097 B 4.80
-// / 5.52 (sweep_final_r2.jsonl), 5121 B 5.64 / 5.47, 7169 B 6.06 / 5.55,
-// 16 385 B 6.32 / 5.19 (sweep_refine, sweep_oddlarge_r2); multiples of 4
-// 8196 B 5.83 / 5.92 (sweep_cross), 10 244 B 6.22 / 6.01, 14 340 B 6.42 /
-// 5.99, 32 772 B 6.62 / 6.18 (profiles/r02/stride/).  The limits sit midway
-// between the last size the stride kernel led and the first it did not.
-// Round 3: with progress priority in one 16-wave workgroup the stride kernel
-// leads odd sizes up to 8.5 KiB (4609 B 5.84 / 5.19 extents, 8193 B 6.10 /
-// 5.70, 8705 B 6.01 / 5.88) and trails from 9 KiB (9217 B 6.04 / 6.11,
-// 10 241 B 6.01 / 6.37; profiles/r03/stride_prio/), so both limits are 9 KiB
-// -- with progress priority.  Without it (PRISKV_CRC_PRIO=0) odd blocks keep
-// round 2's 4.5 KiB limit.  PRISKV_CRC_STRIDE_MAX_KIB sets both (the tests
-// of the kernel's large-block limits).
-constexpr uint32_t kStrideOddMax = 9u << 10;
-constexpr uint32_t kStrideOddMaxNoPrio = 4608;
+// Odd block sizes or bases (not multiples of 4) and other sizes from 9 KiB
+// take the extents kernel: its 16-B aligned windows and one fold per block
+// beat the stride kernel's per-row work once a block spans 9-10 of its rows.
+// Round 2 (profiles/r02/stride/, TB/s extents / stride): odd 4097 B 4.80 /
+// 5.52, 16 385 B 6.32 / 5.19; multiples of 4 14 340 B 6.42 / 5.99.  Round 3,
+// with progress priority in one 16-wave workgroup, the stride kernel leads
+// odd sizes up to 8.5 KiB (4609 B 5.84 / 5.19 extents, 8193 B 6.10 / 5.70,
+// 8705 B 6.01 / 5.88) and trails from 9 KiB (9217 B 6.04 / 6.11, 10 241 B
+// 6.01 / 6.37; profiles/r03/stride_prio/).
 constexpr uint32_t kStrideMax = 9u << 10;
 
-bool stride_to_extents_lim(const void *base, uint32_t bs, uint64_t odd_max, uint64_t max)
+bool stride_to_extents(const void *base, uint32_t bs)
 {
-    const bool odd = (((uintptr_t)base | bs) & 3u) != 0;
-    return bs > kStrideMaxBlock || (odd && bs >= odd_max) || (!odd && bs >= max);
-}
-
-bool stride_to_extents(const priskv_crc_ctx *ctx, const void *base, uint32_t bs)
-{
-    return stride_to_extents_lim(base, bs, ctx->stride_odd_max, ctx->stride_max);
+    (void)base;
+    return bs >= kStrideMax;
 }
 
 // the extents-path kernels a batch of n extents of at most max_len bytes
@@ -1175,118 +1135,72 @@ const char *extents_desc(const priskv_crc_ctx *ctx, uint64_t n, uint64_t max_len
                       : "crc_seg_plan_kernel + crc_ranges_kernel (segments) + crc_seg_reduce_kernel";
 }
 
-StridePlan stride_plan(const priskv_crc_ctx *ctx, uint32_t bs)
+StridePlan stride_plan(uint32_t bs)
 {
     StridePlan best{0, 0};
     double bsc = -1.0;
-    for (int pass = 0; pass < 2 && !best.G; pass++)
-        for (int G = 2; G <= 64; G *= 2) {
-            const uint32_t RB = 16u * (uint32_t)G, R = (uint32_t)(((uint64_t)bs + RB - 1) / RB);
-            if ((G < 16 && R > 1) || (pass == 0 && ctx->stride_g && G != ctx->stride_g))
-                continue;
-            // rows used / rows loaded (half a row of front slack on average),
-            // G <= 16 marked down; from 16 rows of 1 KiB, G = 64 wins outright
-            // (+1-9 % over G = 32 from 16 KiB to 100 KB, -2 % at 12 KiB;
-            // profiles/r02/stride/sweep_large.jsonl) -- such blocks take the
-            // extents kernel unless PRISKV_CRC_STRIDE_MAX_KIB raises the limit
-            const double score = (G == 64 && R >= 16) ? 2.0 : (double)bs / (RB * (R + 0.5)) * (G <= 16 ? 0.88 : 1.0);
-            if (score > bsc) {
-                bsc = score;
-                best = {G, R};
-            }
+    for (int G = 2; G <= 32; G *= 2) {
+        const uint32_t RB = 16u * (uint32_t)G, R = (uint32_t)(((uint64_t)bs + RB - 1) / RB);
+        if (G < 16 && R > 1)
+            continue;
+        // rows used / rows loaded (half a row of front slack on average),
+        // G <= 16 marked down.  (G = 64 never wins below the 9 KiB limit:
+        // 4096 B at an unaligned base G32 0.94 against G64 0.89.)
+        const double score = (double)bs / (RB * (R + 0.5)) * (G <= 16 ? 0.88 : 1.0);
+        if (score > bsc) {
+            bsc = score;
+            best = {G, R};
         }
+    }
     return best;
 }
 
-// workgroups per CU without progress priority: two 8-wave workgroups when
-// their LDS fits (64 KiB image + the nibble tables, 16 KiB for G <= 32; G =
-// 64 needs 32 KiB).  Two gain 18-28 % below 1 KiB, 0-12 % from 1000 to
-// 4097 B over one (profiles/r02/stride/sweep_retune.jsonl, order-rotated).
-int stride_wgs(int G) { return G <= 32 ? 2 : 1; }
-
 // Chunks of 8 rows, 2 in flight (4 x 3, 2 x 4 and 4 x 2 differed by 2-8 %
 // either way with the context order and were dropped: profiles/r02/stride/
-// sweep_tune.jsonl).  odd: a block size or base that is not a multiple of 4
-// -- aligned loads and funnel shifts (unaligned loads stream at
-// 5.3 of 7.0 TB/s).  bf: the byte-table fold (G <= 8).  prio: one 16-wave
-// workgroup per CU with progress-priority mode 3; G >= 16 with aligned loads
-// also requests its first chunks before the tables (256 MiB of 1000-B blocks
-// -2-5 %; the funnel-shift variant lost 5 % at 4097 B and G <= 8 was level:
-// profiles/r03/early/).
+// sweep_tune.jsonl), one 16-wave workgroup per CU with progress-priority
+// mode 3 (round 3: +7-10 % at 1000-6000 B over two 8-wave workgroups).
+// odd: a block size or base that is not a multiple of 4 -- aligned loads and
+// funnel shifts (unaligned loads stream at 5.3 of 7.0 TB/s).
+// G <= 8 (R = 1, set B unused): the byte-table fold in the sub-KiB image.
+// G >= 16 with aligned loads also requests its first chunks before the
+// tables (256 MiB of 1000-B blocks -2-5 %; the funnel-shift variant lost 5 %
+// at 4097 B and G <= 8 was level: profiles/r03/early/).
 template <int G>
-const void *stride_fn_g(bool odd, bool bf, int prio)
+const void *stride_fn_g(bool odd)
 {
-    if constexpr (G >= 16) {
-        if (prio)
-            return odd ? reinterpret_cast<const void *>(&crc_stride_kernel<G, 8, 2, kAux, true, false, 3>)
-                       : reinterpret_cast<const void *>(&crc_stride_kernel<G, 8, 2, kAux, false, false, 3, true>);
-    } else {
-        if (prio && bf)
-            return odd ? reinterpret_cast<const void *>(&crc_stride_kernel<G, 8, 2, kAux, true, true, 3>)
-                       : reinterpret_cast<const void *>(&crc_stride_kernel<G, 8, 2, kAux, false, true, 3>);
-        if (bf) // byte-table fold (R = 1: the B half of the image is free)
-            return odd ? reinterpret_cast<const void *>(&crc_stride_kernel<G, 8, 2, kAux, true, true>)
-                       : reinterpret_cast<const void *>(&crc_stride_kernel<G, 8, 2, kAux, false, true>);
-    }
-    return odd ? reinterpret_cast<const void *>(&crc_stride_kernel<G, 8, 2, kAux, true>)
-               : reinterpret_cast<const void *>(&crc_stride_kernel<G, 8, 2, kAux>);
+    if constexpr (G >= 16)
+        return odd ? reinterpret_cast<const void *>(&crc_stride_kernel<G, 8, 2, kAux, true, false, 3>)
+                   : reinterpret_cast<const void *>(&crc_stride_kernel<G, 8, 2, kAux, false, false, 3, true>);
+    else
+        return odd ? reinterpret_cast<const void *>(&crc_stride_kernel<G, 8, 2, kAux, true, true, 3>)
+                   : reinterpret_cast<const void *>(&crc_stride_kernel<G, 8, 2, kAux, false, true, 3>);
 }
 
-const void *stride_fn(int G, bool odd, bool bf, int prio)
+const void *stride_fn(int G, bool odd)
 {
     switch (G) {
-    case 2: return stride_fn_g<2>(odd, bf, prio);
-    case 4: return stride_fn_g<4>(odd, bf, prio);
-    case 8: return stride_fn_g<8>(odd, bf, prio);
-    case 16: return stride_fn_g<16>(odd, false, prio);
-    case 32: return stride_fn_g<32>(odd, false, prio);
-    default: return stride_fn_g<64>(odd, false, prio);
+    case 2: return stride_fn_g<2>(odd);
+    case 4: return stride_fn_g<4>(odd);
+    case 8: return stride_fn_g<8>(odd);
+    case 16: return stride_fn_g<16>(odd);
+    default: return stride_fn_g<32>(odd);
     }
-}
-
-// Few large odd blocks: the stride kernel splits groups statically like the
-// rows kernel, so an unbalanced handful of big blocks goes to the fused
-// few-extents kernel, which cuts them into segments (as launch_rows does)
-// G <= 8 (R = 1, set B unused): the sub-KiB byte-fold image, no nibble tables
-bool stride_bf(const priskv_crc_ctx *ctx, int G) { return ctx->small_bf && G <= 8; }
-
-// progress priority (mode, 0 = off): one 16-wave workgroup per CU; G <= 8
-// only with the byte fold, whose tables fit the 64 KiB image
-int stride_prio_mode(const priskv_crc_ctx *ctx, int G)
-{
-    return (G >= 16 || stride_bf(ctx, G)) ? ctx->stride_prio : 0;
-}
-
-uint64_t stride_waves(const priskv_crc_ctx *ctx, int G)
-{
-    return stride_prio_mode(ctx, G) ? (uint64_t)ctx->num_cus * 16 : (uint64_t)ctx->num_cus * stride_wgs(G) * kWaves;
-}
-
-bool stride_segmented(const priskv_crc_ctx *ctx, const StridePlan &P, uint64_t nblocks, uint32_t bs)
-{
-    const uint64_t NB = 64 / (uint64_t)P.G;
-    const uint64_t waves = stride_waves(ctx, P.G);
-    return ctx->segment && ctx->fused && bs >= kSegMinLen && nblocks <= kFusedMaxExtents &&
-           !balanced((nblocks + NB - 1) / NB, waves);
 }
 
 int launch_stride(const priskv_crc_ctx *ctx, const uint8_t *base, uint64_t nblocks, uint32_t bs, uint32_t *out,
                   hipStream_t s)
 {
-    const StridePlan P = stride_plan(ctx, bs);
-    if (stride_segmented(ctx, P, nblocks, bs))
-        return launch_fused(ctx, base, nblocks, nullptr, nullptr, bs, bs, out, s);
+    const StridePlan P = stride_plan(bs);
     const uint64_t NB = 64 / (uint64_t)P.G;
-    const bool bf = stride_bf(ctx, P.G);
-    const int prio = stride_prio_mode(ctx, P.G);
-    const uint64_t nw = prio ? 16 : kWaves;
-    const uint64_t max_wgs = prio ? (uint64_t)ctx->num_cus : (uint64_t)ctx->num_cus * stride_wgs(P.G);
+    const bool bf = P.G <= 8;
+    const uint64_t nw = 16;
+    const uint64_t max_wgs = (uint64_t)ctx->num_cus;
     // a wave's range is one buffer descriptor with 31-bit offsets, and its
     // NB lane groups may run up to NB - 1 blocks past it: cap blocks per launch
-    const uint64_t per_wave = ((1ull << 31) - 1) / bs - NB; // >= 1: bs <= kStrideMaxBlock
+    const uint64_t per_wave = ((1ull << 31) - 1) / bs - NB; // >= 1: bs < kStrideMax
     const uint64_t cap = max_wgs * nw * per_wave;
     const uint32_t *img = bf ? ctx->d_small_img[log2u((uint32_t)P.G)]
-                             : ctx->d_lds_image[P.G == 64 ? 0 : (P.G == 32 ? 1 : 2)]; // set B unused for G < 16
+                             : ctx->d_lds_image[P.G == 32 ? 1 : 2]; // set B unused for G < 16
     const uint32_t *nib = ctx->d_nibrep[log2u((uint32_t)P.G)];
     uint32_t R = P.R;
     for (uint64_t done = 0; done < nblocks;) {
@@ -1294,7 +1208,7 @@ int launch_stride(const priskv_crc_ctx *ctx, const uint8_t *base, uint64_t nbloc
         const uint64_t want = (nb + NB * nw - 1) / (NB * nw); // about NB blocks per wave and up
         const uint32_t grid = (uint32_t)(want < max_wgs ? want : max_wgs);
         const uint8_t *b = base + done * bs;
-        const void *fn = stride_fn(P.G, (((uintptr_t)b | bs) & 3u) != 0, bf, prio);
+        const void *fn = stride_fn(P.G, (((uintptr_t)b | bs) & 3u) != 0);
         uint32_t *o = out + done;
         void *args[] = {(void *)&b, (void *)&nb, (void *)&bs, (void *)&R, (void *)&img, (void *)&nib, (void *)&o};
         if (int rc = herr(hipLaunchKernel(fn, dim3(grid), dim3(64 * nw), args, 0, s)))
@@ -1307,33 +1221,32 @@ int launch_stride(const priskv_crc_ctx *ctx, const uint8_t *base, uint64_t nbloc
 int launch_blocks(const priskv_crc_ctx *ctx, const uint8_t *base, uint64_t nblocks, uint32_t bs,
                   uint32_t *out, hipStream_t s)
 {
-    const int path = choose_path(base, bs, ctx->stride);
+    const int path = choose_path(base, bs);
     if (path == PATH_ROWS)
         return launch_rows(ctx, base, nblocks, bs, out, s);
     if (path == PATH_STRIDE && head_split(ctx, base, nblocks, bs))
         return launch_head_split(ctx, base, nblocks, bs, out, s);
-    if (path == PATH_STRIDE && !stride_to_extents(ctx, base, bs))
+    if (path == PATH_STRIDE && !stride_to_extents(base, bs))
         return launch_stride(ctx, base, nblocks, bs, out, s);
-    if (path == PATH_STRIDE) // odd blocks and others from 9 KiB (odd from 4.5 KiB without progress priority),
-                             // beyond 64 MiB: extents (segmented when few)
+    if (path == PATH_STRIDE) // from 9 KiB: extents (segmented when few)
         return launch_extents(ctx, base, nblocks, nullptr, nullptr, bs, bs, out, s);
     if (path == PATH_SMALL) {
         const int gl = log2u(bs / 16); // G = 1 << gl
         const uint64_t per = 1024 / bs; // blocks per row
         const uint64_t nrows = nblocks / per;
         if (nrows) {
-            // G >= 2: nibble-table fold (replicated 32-wide tables)
-            const bool bf = small_bf(ctx, gl);
+            // G = 2..16: byte-table fold (the sub-KiB images), G = 32: nibble-table
+            // fold (replicated 32-wide tables); one 16-wave workgroup per CU
+            const bool bf = gl >= 1 && gl <= 4;
             const uint32_t *fold = gl ? ctx->d_nibrep[gl] : ctx->d_fold;
             const uint32_t *img = bf ? ctx->d_small_img[gl] : ctx->d_lds_image[0];
-            const bool prio = ctx->prio;
-            const int waves = prio ? 2 * kWaves : kWaves;
-            const uint64_t cap = prio ? (uint64_t)ctx->num_cus : (uint64_t)ctx->max_wgs;
-            const uint64_t chw = (uint64_t)(gl == 0 ? kSmallCh1 : prio ? kSmallCh : 4) * waves; // rows per wave-chunk
+            const int waves = 2 * kWaves;
+            const uint64_t cap = (uint64_t)ctx->num_cus;
+            const uint64_t chw = (uint64_t)(gl == 0 ? kSmallCh1 : kSmallCh) * waves; // rows per wave-chunk
             const uint64_t want = (nrows + chw - 1) / chw;
             const uint32_t grid = (uint32_t)(want < cap ? want : cap);
             void *args[] = {(void *)&base, (void *)&nrows, (void *)&img, (void *)&fold, (void *)&out};
-            if (int rc = herr(hipLaunchKernel(small_fn(gl, prio, bf), dim3(grid), dim3(64 * waves), args, 0, s)))
+            if (int rc = herr(hipLaunchKernel(small_fn(gl), dim3(grid), dim3(64 * waves), args, 0, s)))
                 return rc;
         }
         const uint64_t head = nrows * per;
@@ -1407,7 +1320,7 @@ int rows_occupancy(priskv_crc_ctx *c)
 {
     for (int p = 0; p < NPLANS; p++) {
         int n = 0;
-        hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, plan_fn(p, c->prio), 64 * plan_waves(p), 0);
+        hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, plan_fn(p), 64 * plan_waves(p), 0);
         if (e != hipSuccess)
             return herr(e);
         c->plan_wgs_per_cu[p] = n < 1 ? 1 : (n < kPlans[p].wg_per_cu ? n : kPlans[p].wg_per_cu);
@@ -1427,11 +1340,11 @@ int priskv_crc32_blocks_path(const void *d_base, uint64_t nblocks, uint32_t bloc
         return -EINVAL;
     const int path = choose_path(d_base, block_size);
     // a default context hashes B = h + whole KiB rows as bodies + heads
-    // (unless few large blocks), and sends stride sizes from 9 KiB and blocks
-    // beyond 64 MiB to the extents kernel
+    // (unless few large blocks), and sends stride sizes from 9 KiB to the
+    // extents kernel
     if (path == PATH_STRIDE && head_split(nullptr, d_base, nblocks, block_size))
         return PATH_HEAD;
-    if (path == PATH_STRIDE && stride_to_extents_lim(d_base, block_size, kStrideOddMax, kStrideMax))
+    if (path == PATH_STRIDE && stride_to_extents(d_base, block_size))
         return PATH_EXTENTS;
     return path;
 }
@@ -1441,25 +1354,21 @@ int priskv_crc32_blocks_plan(const priskv_crc_ctx *ctx, const void *d_base, uint
 {
     if (!ctx || block_size == 0 || !buf || len == 0)
         return -EINVAL;
-    int path = choose_path(d_base, block_size, ctx->stride);
+    int path = choose_path(d_base, block_size);
     if (path == PATH_STRIDE && head_split(ctx, d_base, nblocks, block_size))
         path = PATH_HEAD;
     int w = 0;
     const char *fused_name = "crc_ranges_fused_kernel (few large values: segments, one launch)";
     if (path == PATH_STRIDE) {
-        const StridePlan P = stride_plan(ctx, block_size);
-        if (stride_to_extents(ctx, d_base, block_size)) {
+        const StridePlan P = stride_plan(block_size);
+        if (stride_to_extents(d_base, block_size)) {
             w = snprintf(buf, len, "%s", extents_desc(ctx, nblocks, block_size));
-        } else if (stride_segmented(ctx, P, nblocks, block_size)) {
-            w = snprintf(buf, len, "%s", fused_name);
         } else {
             const int ch = 8, nbuf = 2;
-            const bool bf = stride_bf(ctx, P.G);
-            const int pm = stride_prio_mode(ctx, P.G);
             w = snprintf(buf, len,
-                         "crc_stride_kernel<G=%d,CH=%d,NBUF=%d,nt%s%s> (%u rows of %u B per block, %u B in front)",
-                         P.G, ch, nbuf, bf ? ",byte-fold" : "", pm ? ",progress-priority 3" : "", P.R, 16u * P.G,
-                         P.R * 16u * P.G - block_size);
+                         "crc_stride_kernel<G=%d,CH=%d,NBUF=%d,nt%s,progress-priority 3> (%u rows of %u B per block, "
+                         "%u B in front)",
+                         P.G, ch, nbuf, P.G <= 8 ? ",byte-fold" : "", P.R, 16u * P.G, P.R * 16u * P.G - block_size);
         }
     } else if (path == PATH_ROWS && segments_for(ctx, nblocks, block_size) > 1 &&
                split_few(ctx, nblocks, block_size) > 1) {
@@ -1468,7 +1377,7 @@ int priskv_crc32_blocks_plan(const priskv_crc_ctx *ctx, const void *d_base, uint
         w = snprintf(buf, len,
                      "crc_rows_kernel<G=64,CH=4,NBUF=3,nt,nibble-fold%s,first chunks before the tables,"
                      "split %u units of %u B per block%s",
-                     ctx->prio ? ",progress-priority 3" : "", sf, block_size / sf, xw ? ",xcd-weighted" : "");
+                     ",progress-priority 3", sf, block_size / sf, xw ? ",xcd-weighted" : "");
         if (w >= 0 && (uint64_t)w < len && xw)
             w += snprintf(buf + w, len - w, " %u:%u", xw >> 16, xw & 0xFFFF);
         if (w >= 0 && (uint64_t)w < len)
@@ -1483,7 +1392,7 @@ int priskv_crc32_blocks_plan(const priskv_crc_ctx *ctx, const void *d_base, uint
         const int p = plan_for(bs, nblocks * S);
         const Plan &P = kPlans[p];
         const uint32_t xw = ctx->plan_xw[p];
-        const int mode = ctx->prio ? (P.opt >> 8) & 3 : 0;
+        const int mode = (P.opt >> 8) & 3;
         w = snprintf(buf, len, "crc_rows_kernel<G=%d,CH=%d,NBUF=%d,nt%s%s", P.G, P.CH, P.NBUF,
                      (P.opt & 2) ? ",pipelined-fold" : "", (P.opt & 32) ? ",nibble-fold" : "");
         if (w >= 0 && (uint64_t)w < len && mode)
@@ -1506,7 +1415,7 @@ int priskv_crc32_blocks_plan(const priskv_crc_ctx *ctx, const void *d_base, uint
             w += snprintf(buf + w, len - w, " on the %u-B bodies + crc_head_kernel (%u-B heads)", block_size, hb);
     } else if (path == PATH_SMALL) {
         const uint32_t G = block_size / 16;
-        w = snprintf(buf, len, "crc_small_kernel<G=%u%s>", G, small_bf(ctx, log2u(G)) ? ",byte-fold" : "");
+        w = snprintf(buf, len, "crc_small_kernel<G=%u%s>", G, (G >= 2 && G <= 16) ? ",byte-fold" : "");
     } else if (path == PATH_EXTENTS) {
         w = snprintf(buf, len, "%s", extents_desc(ctx, nblocks, block_size));
     } else {
@@ -1598,36 +1507,17 @@ int priskv_crc_ctx_create(int device, priskv_crc_ctx **out)
     }
     if ((rc = herr(hipDeviceGetAttribute(&c->num_cus, hipDeviceAttributeMultiprocessorCount, device))))
         goto fail;
-    c->max_wgs = 2 * c->num_cus;
     {
         const char *e = getenv("PRISKV_CRC_SEGMENT");
         c->segment = !(e && !strcmp(e, "0"));
         const char *sp = getenv("PRISKV_CRC_SPLIT");
         c->split = !(sp && !strcmp(sp, "0"));
-        const char *pe = getenv("PRISKV_CRC_PRIO");
-        c->prio = !(pe && !strcmp(pe, "0"));
         const char *be = getenv("PRISKV_CRC_BALANCE");
         c->balance = !(be && !strcmp(be, "0"));
         const char *hs = getenv("PRISKV_CRC_HEADSPLIT");
         c->head_split = !(hs && !strcmp(hs, "0"));
-        const char *sb = getenv("PRISKV_CRC_SMALL_BF");
-        c->small_bf = !(sb && !strcmp(sb, "0"));
         const char *fe = getenv("PRISKV_CRC_FUSED");
         c->fused = !(fe && !strcmp(fe, "0"));
-        const char *fx = getenv("PRISKV_CRC_FUSED_XW");
-        c->fused_xw = !(fx && !strcmp(fx, "0"));
-        const char *se = getenv("PRISKV_CRC_STRIDE");
-        c->stride = !(se && !strcmp(se, "0"));
-        c->stride_g = 0;
-        if (const char *m = getenv("PRISKV_CRC_STRIDE_G")) {
-            const int v = atoi(m);
-            c->stride_g = (v >= 2 && v <= 64 && !(v & (v - 1))) ? v : 0;
-        }
-        c->stride_prio = c->prio ? 3 : 0; // PRISKV_CRC_PRIO=0 turns it off with the others
-        c->stride_max = kStrideMax;
-        c->stride_odd_max = c->stride_prio ? kStrideOddMax : kStrideOddMaxNoPrio;
-        if (const char *m = getenv("PRISKV_CRC_STRIDE_MAX_KIB"))
-            c->stride_max = c->stride_odd_max = strtoull(m, nullptr, 10) << 10;
         c->seg_max_extents = kSegMaxExtents;
         c->tile_min_bytes = kTileMinBytes;
         c->tile_bytes = kTileBytes;

@@ -52,38 +52,18 @@ def ctx_noseg(torch_cuda):
     c.close()
 
 
-@pytest.fixture(scope="module")
-def ctx_noprio(torch_cuda):
-    """A context with the rows kernel's progress priority off
-    (PRISKV_CRC_PRIO=0, read at creation)."""
-    import os
-    from priskv_amd import CrcContext
-    old = os.environ.get("PRISKV_CRC_PRIO")
-    os.environ["PRISKV_CRC_PRIO"] = "0"
-    try:
-        c = CrcContext(0)
-    finally:
-        if old is None:
-            del os.environ["PRISKV_CRC_PRIO"]
-        else:
-            os.environ["PRISKV_CRC_PRIO"] = old
-    yield c
-    c.close()
-
-
 @pytest.mark.parametrize("bs", [16, 32, 64, 128, 256, 512, 1024, 3072, 4096, 8192, 65536, 131072, 262144, 1 << 20])
-def test_progress_priority_on_and_off(torch_cuda, ctx, ctx_noprio, bs):
-    """Every rows plan and the sub-KiB kernel with and without progress
-    priority (and, sub-KiB, its 16-wave shape): the same CRCs as the oracle
-    (priority only reorders instruction issue)."""
+def test_every_plan_at_48MiB(torch_cuda, ctx, bs):
+    """Every rows plan and the sub-KiB kernel at ~48 MiB per call, a ragged
+    count: the oracle's CRCs.  (Round 5 removed the no-priority variants,
+    PRISKV_CRC_PRIO=0, measured slower in rounds 1-3.)"""
     torch = torch_cuda
     nb = max(1, (48 << 20) // bs) + 3
     t = _region(torch, ctx, bs * nb, SEED ^ (bs * 7), nb)
     want = O.crc32_blocks(t[: bs * nb].cpu().numpy(), bs, nthreads=8)
-    for c in (ctx, ctx_noprio):
-        got = _u32(c.blocks_dev(t, bs, nblocks=nb))
-        torch.cuda.synchronize()
-        assert np.array_equal(got, want), (bs, nb, np.nonzero(got != want)[0][:8])
+    got = _u32(ctx.blocks_dev(t, bs, nblocks=nb))
+    torch.cuda.synchronize()
+    assert np.array_equal(got, want), (bs, nb, np.nonzero(got != want)[0][:8])
 
 
 @pytest.fixture(scope="module")
@@ -140,11 +120,10 @@ def test_segmentation_limit_boundary(torch_cuda, ctx):
         assert np.array_equal(got, want), (k, np.nonzero(got != want)[0][:8])
 
 
-@pytest.fixture(params=["segmented", "unsegmented", "no-priority"])
-def any_ctx(request, ctx, ctx_noseg, ctx_noprio):
-    """The default context, one with segmentation off, and one with the
-    progress priority off (rows and extents kernels)."""
-    return {"segmented": ctx, "unsegmented": ctx_noseg, "no-priority": ctx_noprio}[request.param]
+@pytest.fixture(params=["segmented", "unsegmented"])
+def any_ctx(request, ctx, ctx_noseg):
+    """The default context and one with segmentation off."""
+    return {"segmented": ctx, "unsegmented": ctx_noseg}[request.param]
 
 
 def _region(torch, ctx, nbytes, seed=SEED, word_offset=0, pad=0):
@@ -216,28 +195,24 @@ def test_blocks_vs_oracle(torch_cuda, ctx, bs):
         assert np.array_equal(got, want), (bs, nb, np.nonzero(got != want)[0][:8])
 
 
-@pytest.mark.parametrize("bf", ["1", "0"])
-def test_sub_kib_fold_tables(torch_cuda, bf):
-    """crc_small_kernel with the byte-table fold (default) and the nibble
-    fold (PRISKV_CRC_SMALL_BF=0) against the oracle, every sub-KiB power of
-    two, whole and ragged rows (the ragged tail takes the generic kernel)."""
+def test_sub_kib_fold_tables(torch_cuda, ctx):
+    """crc_small_kernel (byte-table fold for G = 2..16, nibble fold at G = 32,
+    none at G = 1) against the oracle, every sub-KiB power of two, whole and
+    ragged rows (the ragged tail takes the generic kernel)."""
     torch = torch_cuda
-    c = _ctx_env(PRISKV_CRC_SMALL_BF=bf)
-    try:
-        for bs in (16, 32, 64, 128, 256, 512):
-            plan = c.blocks_plan(16, 4096, bs)
-            assert plan.startswith(f"crc_small_kernel<G={bs // 16}"), plan
-            assert ("byte-fold" in plan) == (bf == "1" and 32 <= bs <= 256), plan
-            for nb in (1024 // bs * 3 * 2048 * 16 + 1, 1024 // bs * 40 + 3, 1024 // bs * 256 * 16 * 4 * 5 + 7):
-                t = _region(torch, c, bs * nb, SEED ^ (bs * 7 + nb), nb)
-                out = torch.full((nb,), 0x5A5A5A5A, dtype=torch.int32, device="cuda")
-                got = _u32(c.blocks_dev(t, bs, out=out, nblocks=nb))
-                torch.cuda.synchronize()
-                want = O.crc32_blocks(t[: bs * nb].cpu().numpy(), bs, nthreads=8)
-                assert np.array_equal(got, want), (bf, bs, nb, np.nonzero(got != want)[0][:8])
-                del t
-    finally:
-        c.close()
+    c = ctx
+    for bs in (16, 32, 64, 128, 256, 512):
+        plan = c.blocks_plan(16, 4096, bs)
+        assert plan.startswith(f"crc_small_kernel<G={bs // 16}"), plan
+        assert ("byte-fold" in plan) == (32 <= bs <= 256), plan
+        for nb in (1024 // bs * 3 * 2048 * 16 + 1, 1024 // bs * 40 + 3, 1024 // bs * 256 * 16 * 4 * 5 + 7):
+            t = _region(torch, c, bs * nb, SEED ^ (bs * 7 + nb), nb)
+            out = torch.full((nb,), 0x5A5A5A5A, dtype=torch.int32, device="cuda")
+            got = _u32(c.blocks_dev(t, bs, out=out, nblocks=nb))
+            torch.cuda.synchronize()
+            want = O.crc32_blocks(t[: bs * nb].cpu().numpy(), bs, nthreads=8)
+            assert np.array_equal(got, want), (bs, nb, np.nonzero(got != want)[0][:8])
+            del t
 
 
 @pytest.mark.parametrize("misalign", [1, 2, 4, 8, 12, 15])
@@ -1359,10 +1334,6 @@ def test_blocks_plan_strings(torch_cuda, ctx):
     assert ctx.blocks_plan(base, 100, 9300) == "crc_ranges_kernel (extents)"
     assert "crc_head_kernel (4-B heads)" in ctx.blocks_plan(base, 100, 9220)
     assert ctx.blocks_plan(base, 100, 15) == "crc_generic_kernel"
-    off =_ctx_env(PRISKV_CRC_STRIDE="0")  # round 2's dispatch
-    assert off.blocks_plan(base + 1, 100, 4096) == "crc_ranges_kernel (extents)"
-    assert off.blocks_plan(base, 100, 100) == "crc_generic_kernel"
-    off.close()
 
 
 def test_ranges_host_concurrent_temporary_registration(torch_cuda):
@@ -1528,16 +1499,6 @@ def ctx_fused16k(torch_cuda):
     c.close()
 
 
-@pytest.fixture(scope="module")
-def ctx_fused_variants(torch_cuda):
-    """The fused kernel without its XCD-weighted finer split
-    (PRISKV_CRC_FUSED_XW=0: round 3's 16 KiB segments, count split)."""
-    cs = [_ctx_env(PRISKV_CRC_SEG_MAX_EXTENTS=16384, PRISKV_CRC_FUSED_XW=0)]
-    yield cs
-    for c in cs:
-        c.close()
-
-
 _FUSED_CASES = [
     [256 << 20],                                  # a lone huge value: every workgroup holds part of it
     [(1 << 14) + 1],                              # two segments, the last one byte
@@ -1555,7 +1516,7 @@ _FUSED_CASES = [
 
 
 @pytest.mark.parametrize("case", range(len(_FUSED_CASES) + 2))
-def test_fused_few_extents(torch_cuda, ctx_fused16k, ctx_threelaunch, ctx_fused_variants, case):
+def test_fused_few_extents(torch_cuda, ctx_fused16k, ctx_threelaunch, case):
     """The one-launch few-extents kernel (plan in LDS, per-extent counters,
     last-arriver combine) equals the oracle and the three-launch path, at
     ragged offsets on a 16-B-misaligned base, called repeatedly (the counters
@@ -1582,7 +1543,7 @@ def test_fused_few_extents(torch_cuda, ctx_fused16k, ctx_threelaunch, ctx_fused_
     d_o = torch.from_numpy(o.astype(np.int64)).cuda()
     d_l = torch.from_numpy(lens.view(np.int32)).cuda()
     want = O.crc32_ranges(base[:n].cpu().numpy(), o, lens)
-    for c in [ctx_fused16k, ctx_threelaunch] + ctx_fused_variants:
+    for c in [ctx_fused16k, ctx_threelaunch]:
         for _ in range(3):
             got = _u32(c.ranges_dev(base, d_o, d_l))
             torch.cuda.synchronize()
@@ -1641,55 +1602,39 @@ def test_fused_single_value_beyond_2GiB(torch_cuda, ctx, kind):
     torch.cuda.empty_cache()
 
 
-# (G, block sizes the forced G can take): G < 16 only with one row per block
+# (G, block sizes whose cost-model plan is G lanes per block): G < 16 only
+# with one row per block; G = 64 never wins below the 9 KiB limit
 _STRIDE_SIZES = {2: [16, 17, 23, 32], 4: [33, 48, 50, 64], 8: [65, 100, 127, 128],
-                 16: [129, 255, 257, 1000, 4100, 65537], 32: [257, 511, 1000, 4097, 12345],
-                 64: [513, 1023, 1025, 3000, 100003]}
+                 16: [129, 255, 257, 520, 700], 32: [769, 1000, 1023, 4097, 8193, 9215]}
 
 
 @pytest.mark.parametrize("G", sorted(_STRIDE_SIZES))
-def test_stride_kernel_every_g_and_variant(torch_cuda, G):
+def test_stride_kernel_every_g_and_variant(torch_cuda, ctx, G):
     """crc_stride_kernel (odd block sizes, unaligned bases) for every lane
-    count G (forced, PRISKV_CRC_STRIDE_G) and every variant the library
-    ships: progress priority in one 16-wave workgroup or two 8-wave
-    workgroups (PRISKV_CRC_PRIO=0), byte or nibble fold (G <= 8,
-    PRISKV_CRC_SMALL_BF=0), aligned or funnel-shift loads: the oracle's CRCs
-    at base misalignments 0, 3 and 4, for batches of 1 block, a ragged last
-    group, and several groups per wave with a ragged end."""
+    count G the cost model picks, byte fold (G <= 8) or nibble fold, aligned
+    or funnel-shift loads: the oracle's CRCs at base misalignments 0, 3 and
+    4, for batches of 1 block, a ragged last group, and several groups per
+    wave with a ragged end.  (Round 5 removed the forced-G and size-limit
+    test hooks and the measured-slower variants they reached.)"""
     torch = torch_cuda
-    hs = {"PRISKV_CRC_HEADSPLIT": 0}  # 4100 B and the like stay on the stride kernel
-    ctxs = [_ctx_env(PRISKV_CRC_STRIDE_G=G, **hs),
-            _ctx_env(PRISKV_CRC_STRIDE_G=G, PRISKV_CRC_SMALL_BF=0, **hs),  # G <= 8: nibble fold
-            _ctx_env(PRISKV_CRC_STRIDE_G=G, PRISKV_CRC_PRIO=0, **hs),  # two 8-wave workgroups
-            _ctx_env(PRISKV_CRC_STRIDE_G=G, PRISKV_CRC_PRIO=0, PRISKV_CRC_SMALL_BF=0, **hs),
-            _ctx_env(PRISKV_CRC_STRIDE_G=G, PRISKV_CRC_STRIDE_MAX_KIB=131072, **hs)]  # large blocks stay here
     per = 64 // G
     rng = np.random.default_rng(G)
-    try:
-        for bs in _STRIDE_SIZES[G]:
-            big = max(per + 1, min((24 << 20) // bs, 3 * 2048 * per + per // 2 + 1))
-            for nb in (1, per + 1, big):
-                fast = bs % 1024 == 0 or (bs & (bs - 1) == 0 and bs <= 512)  # aligned: rows / sub-KiB kernels
-                mis = int(rng.choice([3, 4] if fast else [0, 3, 4]))
-                t = _region(torch, ctxs[0], bs * nb + 16, SEED ^ (bs * 131 + nb), nb)
-                view = t[mis: mis + bs * nb]
-                want = O.crc32_blocks(view.cpu().numpy(), bs, nthreads=8)
-                for sh, c in enumerate(ctxs):
-                    plan = c.blocks_plan(view.data_ptr(), nb, bs)
-                    # a few unbalanced blocks >= 64 KiB are cut into segments by the fused
-                    # kernel; sizes from 9 KiB take the extents kernel
-                    odd_big = bs >= 9216 and c is not ctxs[-1]
-                    assert plan.startswith(f"crc_stride_kernel<G={G},") or (
-                        bs >= 65536 and plan.startswith("crc_ranges_fused_kernel")) or (
-                        odd_big and plan.startswith("crc_ranges_kernel")), plan
-                    # a sentinel-filled output: a CRC the kernel fails to store shows
-                    out = torch.full((nb,), 0x5A5A5A5A, dtype=torch.int32, device="cuda")
-                    got = _u32(c.blocks_dev(view, bs, out=out, nblocks=nb))
-                    torch.cuda.synchronize()
-                    assert np.array_equal(got, want), (G, sh, bs, nb, mis, np.nonzero(got != want)[0][:8])
-    finally:
-        for c in ctxs:
-            c.close()
+    for bs in _STRIDE_SIZES[G]:
+        big = max(per + 1, min((24 << 20) // bs, 3 * 2048 * per + per // 2 + 1))
+        for nb in (1, per + 1, big):
+            fast = bs % 1024 == 0 or (bs & (bs - 1) == 0 and bs <= 512)  # aligned: rows / sub-KiB kernels
+            mis = int(rng.choice([3, 4] if fast else [0, 3, 4]))
+            t = _region(torch, ctx, bs * nb + 16, SEED ^ (bs * 131 + nb), nb)
+            view = t[mis: mis + bs * nb]
+            want = O.crc32_blocks(view.cpu().numpy(), bs, nthreads=8)
+            plan = ctx.blocks_plan(view.data_ptr(), nb, bs)
+            assert plan.startswith(f"crc_stride_kernel<G={G},"), plan
+            # a sentinel-filled output: a CRC the kernel fails to store shows
+            out = torch.full((nb,), 0x5A5A5A5A, dtype=torch.int32, device="cuda")
+            got = _u32(ctx.blocks_dev(view, bs, out=out, nblocks=nb))
+            torch.cuda.synchronize()
+            assert np.array_equal(got, want), (G, bs, nb, mis, np.nonzero(got != want)[0][:8])
+            del t
 
 
 @pytest.mark.parametrize("misalign", [0, 1, 2, 3, 4, 8, 13])
@@ -1734,34 +1679,26 @@ def test_stride_kernel_beyond_4GiB(torch_cuda, ctx):
     torch.cuda.empty_cache()
 
 
-# noseg: segmentation off; wide: PRISKV_CRC_STRIDE_MAX_KIB = 128 MiB, so
-# blocks that are multiples of 4 from 16 KiB stay on the stride kernel
-@pytest.mark.parametrize("bs,nb,mis,kind,noseg,wide", [((64 << 20) - 3, 3, 1, "crc_ranges_fused_kernel", False, False),
-                                                     ((64 << 20) - 4, 3, 4, "crc_stride_kernel<G=64,", True, True),
-                                                     ((64 << 20) - 4, 3, 4, "crc_ranges_kernel (extents)", True, False),
-                                                     ((64 << 20) + 5, 2, 0, "crc_ranges_fused_kernel", False, False),
-                                                     ((5 << 20) + 8, 400, 4, "crc_stride_kernel<G=64,", True, True),
-                                                     ((5 << 20) + 7, 400, 2, "crc_ranges_kernel (extents)", True,
-                                                      False),
-                                                     (4607, 6000, 1, "crc_stride_kernel<G=32,", False, False),
-                                                     (4609, 6000, 0, "crc_stride_kernel<G=32,", False, False),
-                                                     (9217, 3000, 0, "crc_ranges_kernel (extents)", False, False),
-                                                     (16460, 3000, 0, "crc_ranges_kernel (extents)", False, False),
-                                                     (16388, 3000, 0, "crc_rows_kernel<G=64,", False, False),
-                                                     (4100, 2049, 4, "crc_rows_kernel<G=64,", False, False)])
-def test_stride_kernel_large_and_limit_blocks(torch_cuda, ctx, ctx_noseg, bs, nb, mis, kind, noseg, wide):
-    """Blocks at both sides of the stride kernel's limits: 64 MiB (a few such
-    blocks are cut into segments by the fused kernel, or with segmentation
-    off and the size limit raised hashed whole by the stride kernel: 65 536
-    rows of 1 KiB; more than 64 MiB keeps the extents path), 9 KiB (the
-    extents kernel from there), 2 GB
-    batches of 5 MiB + 8 / + 7 B blocks, a batch whose last lane-group runs
-    are short, and sizes of whole KiB rows + a 4-B head, which the head split
-    hands to the rows kernel: the oracle's CRCs."""
+# noseg: segmentation off
+@pytest.mark.parametrize("bs,nb,mis,kind,noseg", [((64 << 20) - 3, 3, 1, "crc_ranges_fused_kernel", False),
+                                               ((64 << 20) - 4, 3, 4, "crc_ranges_kernel (extents)", True),
+                                               ((64 << 20) + 5, 2, 0, "crc_ranges_fused_kernel", False),
+                                               ((5 << 20) + 7, 400, 2, "crc_ranges_kernel (extents)", True),
+                                               (4607, 6000, 1, "crc_stride_kernel<G=32,", False),
+                                               (4609, 6000, 0, "crc_stride_kernel<G=32,", False),
+                                               (9217, 3000, 0, "crc_ranges_kernel (extents)", False),
+                                               (16460, 3000, 0, "crc_ranges_kernel (extents)", False),
+                                               (16388, 3000, 0, "crc_rows_kernel<G=64,", False),
+                                               (4100, 2049, 4, "crc_rows_kernel<G=64,", False)])
+def test_stride_kernel_large_and_limit_blocks(torch_cuda, ctx, ctx_noseg, bs, nb, mis, kind, noseg):
+    """Blocks at both sides of the stride kernel's 9 KiB limit and far past
+    it: 64 MiB (a few such blocks are cut into segments by the fused kernel,
+    or with segmentation off hashed whole by the extents kernel), 2 GB
+    batches of 5 MiB + 7 B blocks, and sizes of whole KiB rows + a 4-B
+    head, which the head split hands to the rows kernel: the oracle's
+    CRCs."""
     torch = torch_cuda
     ctx = ctx_noseg if noseg else ctx
-    if wide:
-        ctx = _ctx_env(PRISKV_CRC_SEGMENT="0", PRISKV_CRC_STRIDE_MAX_KIB=131072, PRISKV_CRC_HEADSPLIT=0)
     t = _region(torch, ctx, bs * nb + 16, SEED ^ (bs + nb), 5)
     view = t[mis: mis + bs * nb]
     plan = ctx.blocks_plan(view.data_ptr(), nb, bs)
@@ -1770,7 +1707,5 @@ def test_stride_kernel_large_and_limit_blocks(torch_cuda, ctx, ctx_noseg, bs, nb
     torch.cuda.synchronize()
     want = O.crc32_blocks(view.cpu().numpy(), bs, nthreads=16)
     assert np.array_equal(got, want), (bs, nb, np.nonzero(got != want)[0][:8])
-    if wide:
-        ctx.close()
     del t, view
     torch.cuda.empty_cache()
