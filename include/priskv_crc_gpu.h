@@ -201,7 +201,10 @@ int priskv_crc_fill_splitmix_dev(const priskv_crc_ctx *ctx, void *d_dst, uint64_
  * whole KiB rows plus a 4-64 B head, 4-byte aligned base: the rows kernel on
  * the bodies, then the heads' terms; not for a batch of few blocks with
  * bodies of 64 KiB and more, which the extents path segments -- judged for a
- * 256-CU device).  The exact kernels a given context launches, few-block
+ * 256-CU device), 7 = window (any other block within W - 15 .. W + 48 B
+ * of a multiple W of 4 KiB up to 16 KiB -- 4095, 4097, 8193 B, 4096 B on an
+ * odd base: the rows kernel on each block's 16-B aligned W-byte window, then
+ * the few bytes where window and block differ).  The exact kernels a given context launches, few-block
  * segmentation included, are reported by
  * priskv_crc32_blocks_plan.  For tests and benchmarks; -EINVAL for invalid
  * arguments. */

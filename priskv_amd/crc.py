@@ -25,9 +25,9 @@ import numpy as np
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "lib", "libpriskv_crc.so")
 
-PATH_ROWS, PATH_EXTENTS, PATH_SMALL, PATH_GENERIC, PATH_STRIDE, PATH_HEAD = 1, 2, 3, 4, 5, 6
+PATH_ROWS, PATH_EXTENTS, PATH_SMALL, PATH_GENERIC, PATH_STRIDE, PATH_HEAD, PATH_WINDOW = 1, 2, 3, 4, 5, 6, 7
 PATH_NAMES = {PATH_ROWS: "rows", PATH_EXTENTS: "extents", PATH_SMALL: "small", PATH_GENERIC: "generic",
-              PATH_STRIDE: "stride", PATH_HEAD: "headsplit"}
+              PATH_STRIDE: "stride", PATH_HEAD: "headsplit", PATH_WINDOW: "window"}
 
 _lib: Optional[ctypes.CDLL] = None
 

@@ -75,6 +75,7 @@ struct priskv_crc_ctx {
     int split;                 // rows kernel split mode for few blocks per wave (PRISKV_CRC_SPLIT=0: off)
     int balance;               // byte-balanced extents split (PRISKV_CRC_BALANCE=0: off)
     int head_split;            // rows kernel + head terms for B = h + whole KiB rows (PRISKV_CRC_HEADSPLIT=0: off)
+    int window;                // rows kernel on 16-B aligned windows for sizes near 4 KiB multiples (PRISKV_CRC_WINDOW=0: off)
     uint64_t seg_max_extents;  // device-resident lengths: segment calls of at most this many extents
     int xcd_rr;                // the XCD probe found round-robin dispatch: workgroup b on XCD (b + k) % 8 (weights apply)
     uint64_t tile_min_bytes;   // rows batches of at least this many bytes run in block-cyclic tiles
@@ -407,7 +408,15 @@ struct Scratch {
 
 inline bool is_pow2(uint64_t v) { return v && !(v & (v - 1)); }
 
-enum Path { PATH_ROWS = 1, PATH_EXTENTS = 2, PATH_SMALL = 3, PATH_GENERIC = 4, PATH_STRIDE = 5, PATH_HEAD = 6 };
+enum Path {
+    PATH_ROWS = 1,
+    PATH_EXTENTS = 2,
+    PATH_SMALL = 3,
+    PATH_GENERIC = 4,
+    PATH_STRIDE = 5,
+    PATH_HEAD = 6,
+    PATH_WINDOW = 7
+};
 
 int choose_path(const void *d_base, uint32_t block_size)
 {
@@ -1056,6 +1065,82 @@ int launch_head_split(const priskv_crc_ctx *ctx, const uint8_t *base, uint64_t n
     return launch_k(crc_head_kernel, dim3(grid), dim3(256), s, base, nblocks, bs, h, ctx->d_sarwate, z, out);
 }
 
+// ---- window blocks -------------------------------------------------------------
+// A block size B within [W - 15, W + 48] of a multiple W of 4 KiB (W <= 16
+// KiB) that is odd or on an odd base -- 4095, 4097, 8193 B, 4096 B at base
+// + 1: the rows kernel hashes each block's window, the W bytes that end at
+// the first 16-B boundary at or after the block's end (crc_rows_kernel OPT
+// bit 13: aligned 1 KiB rows at W's plan, one chunk cursor jump per block),
+// and crc_window_fix_kernel trades the at most 15 + 63 bytes where window and
+// block differ.  The head split goes first (4-byte aligned
+// B = h + whole KiB rows).
+// PRISKV_CRC_WINDOW=0 turns it off (the stride kernel / extents path).
+constexpr uint32_t kWinMaxBytes = 16u << 10, kWinOver = 48;
+constexpr int kWinOpt = 8192;
+
+uint32_t window_bytes(const priskv_crc_ctx *ctx, const void *base, uint64_t nblocks, uint32_t bs)
+{
+    const uint32_t W = (uint32_t)(((uint64_t)bs + 15) / 4096 * 4096); // W - 15 <= bs
+    (void)base;
+    (void)nblocks; // (blocks this small are never segmented: kSegMinLen)
+    static_assert(kWinMaxBytes + kWinOver < kSegMinLen, "window sizes are never segmented");
+    return ((ctx && !ctx->window) || W == 0 || W > kWinMaxBytes || bs > W + kWinOver) ? 0u : W;
+}
+
+template <int P>
+const void *window_kernel_p()
+{
+    constexpr Plan Q = kPlans[P];
+    static_assert(Q.G == 64, "window mode: one block per wave group");
+    return plan_kernel<Q.G, Q.CH, Q.NBUF, Q.opt | kWinOpt>();
+}
+
+const void *window_fn(int p)
+{
+    switch (p) {
+    case PLAN_4K: return window_kernel_p<PLAN_4K>();
+    case PLAN_4K_DEEP: return window_kernel_p<PLAN_4K_DEEP>();
+    case PLAN_G64_CH4_NIB: return window_kernel_p<PLAN_G64_CH4_NIB>();
+    default: return window_kernel_p<PLAN_G64_CH4>();
+    }
+}
+
+int launch_window(const priskv_crc_ctx *ctx, const uint8_t *base, uint64_t nblocks, uint32_t bs, uint32_t W,
+                  uint32_t *out, hipStream_t s)
+{
+    const int p = plan_for(W, nblocks); // 4 KiB, 4 KiB deep, 8 KiB or the G64 CH4 plan
+    const Plan &P = kPlans[p];
+    const uint64_t max_wgs = (uint64_t)ctx->num_cus * ctx->plan_wgs_per_cu[p];
+    const uint64_t NW = (uint64_t)plan_waves(p);
+    const uint64_t cps = W / ((uint64_t)P.CH * 16u * P.G);
+    const uint32_t *img = ctx->d_lds_image[0];
+    const uint32_t *fold = (P.opt & 32) ? ctx->d_nibrep[6] : ctx->d_fold + 6 * 2048;
+    const uint32_t *zp = ctx->d_zpow;
+    const uint64_t cap = max_wgs * NW * ((1ull << 31) / cps - 1);
+    for (uint64_t done = 0; done < nblocks;) {
+        uint64_t n = (nblocks - done < cap) ? nblocks - done : cap;
+        const uint64_t want = (n + NW - 1) / NW;
+        const uint32_t grid = (uint32_t)(want < max_wgs ? want : max_wgs);
+        const uint8_t *b = base + done * bs;
+        uint32_t *o = out + done;
+        uint32_t xw = n >= 32ull * grid * NW ? ctx->plan_xw[p] : 0u, tile = 0, one = 1, stride = bs, wb = W;
+        uint32_t *none = nullptr;
+        void *args[] = {(void *)&b,  (void *)&n,    (void *)&wb,   (void *)&img,    (void *)&fold,
+                        (void *)&o,  (void *)&xw,   (void *)&tile, (void *)&stride, (void *)&one,
+                        (void *)&zp, (void *)&none, (void *)&none};
+        if (int rc = herr(hipLaunchKernel(window_fn(p), dim3(grid), dim3(64 * NW), args, 0, s)))
+            return rc;
+        done += n;
+    }
+    HeadCols z, z16;
+    prv_shift_columns(z.c, W);
+    prv_shift_columns(z16.c, W - 16);
+    const uint64_t want = (nblocks + 255) / 256;
+    const uint32_t grid = (uint32_t)(want < (uint64_t)ctx->num_cus * 8 ? want : (uint64_t)ctx->num_cus * 8);
+    return launch_k(crc_window_fix_kernel, dim3(grid), dim3(256), s, base, nblocks, bs, W, ctx->d_sarwate,
+                    ctx->d_rowshift, z, z16, out);
+}
+
 // sub-KiB kernel for G = 1 << gl: no fold at G = 1 (a lane holds a whole
 // block); G = 2-16 the byte-table fold, G = 32 the nibble fold; with prio in
 // one 16-wave workgroup per CU and progress-priority mode 1 (+0.2-2.6 % at
@@ -1226,6 +1311,9 @@ int launch_blocks(const priskv_crc_ctx *ctx, const uint8_t *base, uint64_t nbloc
         return launch_rows(ctx, base, nblocks, bs, out, s);
     if (path == PATH_STRIDE && head_split(ctx, base, nblocks, bs))
         return launch_head_split(ctx, base, nblocks, bs, out, s);
+    if (path == PATH_STRIDE)
+        if (const uint32_t W = window_bytes(ctx, base, nblocks, bs))
+            return launch_window(ctx, base, nblocks, bs, W, out, s);
     if (path == PATH_STRIDE && !stride_to_extents(base, bs))
         return launch_stride(ctx, base, nblocks, bs, out, s);
     if (path == PATH_STRIDE) // from 9 KiB: extents (segmented when few)
@@ -1344,6 +1432,8 @@ int priskv_crc32_blocks_path(const void *d_base, uint64_t nblocks, uint32_t bloc
     // extents kernel
     if (path == PATH_STRIDE && head_split(nullptr, d_base, nblocks, block_size))
         return PATH_HEAD;
+    if (path == PATH_STRIDE && window_bytes(nullptr, d_base, nblocks, block_size))
+        return PATH_WINDOW;
     if (path == PATH_STRIDE && stride_to_extents(d_base, block_size))
         return PATH_EXTENTS;
     return path;
@@ -1357,9 +1447,18 @@ int priskv_crc32_blocks_plan(const priskv_crc_ctx *ctx, const void *d_base, uint
     int path = choose_path(d_base, block_size);
     if (path == PATH_STRIDE && head_split(ctx, d_base, nblocks, block_size))
         path = PATH_HEAD;
+    const uint32_t win = path == PATH_STRIDE ? window_bytes(ctx, d_base, nblocks, block_size) : 0u;
     int w = 0;
     const char *fused_name = "crc_ranges_fused_kernel (few large values: segments, one launch)";
-    if (path == PATH_STRIDE) {
+    if (win) {
+        const int p = plan_for(win, nblocks);
+        const Plan &P = kPlans[p];
+        w = snprintf(buf, len,
+                     "crc_rows_kernel<G=%d,CH=%d,NBUF=%d,nt%s%s,progress-priority %d,window> (%u-B windows ending at "
+                     "the 16-B boundary after each block) + crc_window_fix_kernel",
+                     P.G, P.CH, P.NBUF, (P.opt & 2) ? ",pipelined-fold" : "", (P.opt & 32) ? ",nibble-fold" : "",
+                     (P.opt >> 8) & 3, win);
+    } else if (path == PATH_STRIDE) {
         const StridePlan P = stride_plan(block_size);
         if (stride_to_extents(d_base, block_size)) {
             w = snprintf(buf, len, "%s", extents_desc(ctx, nblocks, block_size));
@@ -1516,6 +1615,8 @@ int priskv_crc_ctx_create(int device, priskv_crc_ctx **out)
         c->balance = !(be && !strcmp(be, "0"));
         const char *hs = getenv("PRISKV_CRC_HEADSPLIT");
         c->head_split = !(hs && !strcmp(hs, "0"));
+        const char *we = getenv("PRISKV_CRC_WINDOW");
+        c->window = !(we && !strcmp(we, "0"));
         const char *fe = getenv("PRISKV_CRC_FUSED");
         c->fused = !(fe && !strcmp(fe, "0"));
         c->seg_max_extents = kSegMaxExtents;

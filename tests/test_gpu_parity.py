@@ -1605,7 +1605,7 @@ def test_fused_single_value_beyond_2GiB(torch_cuda, ctx, kind):
 # (G, block sizes whose cost-model plan is G lanes per block): G < 16 only
 # with one row per block; G = 64 never wins below the 9 KiB limit
 _STRIDE_SIZES = {2: [16, 17, 23, 32], 4: [33, 48, 50, 64], 8: [65, 100, 127, 128],
-                 16: [129, 255, 257, 520, 700], 32: [769, 1000, 1023, 4097, 8193, 9215]}
+                 16: [129, 255, 257, 520, 700], 32: [769, 1000, 1023, 4200, 8301, 9215]}
 
 
 @pytest.mark.parametrize("G", sorted(_STRIDE_SIZES))
@@ -1654,6 +1654,45 @@ def test_stride_kernel_cost_model_sizes(torch_cuda, ctx, misalign):
         torch.cuda.synchronize()
         want = O.crc32_blocks(view.cpu().numpy(), bs, nthreads=8)
         assert np.array_equal(got, want), (bs, nb, misalign, np.nonzero(got != want)[0][:8])
+
+
+# block sizes within W - 15 .. W + 48 B of W = 4, 8, 12, 16 KiB: window mode
+_WINDOW_SIZES = [4081, 4095, 4096, 4097, 4099, 4111, 4112, 4127, 4144, 8177, 8191, 8193, 8240, 12287, 12300,
+                 16369, 16383, 16385, 16432]
+
+
+@pytest.mark.parametrize("bs", _WINDOW_SIZES)
+def test_window_blocks(torch_cuda, ctx, bs):
+    """Odd sizes (or 4 KiB on odd bases) near a multiple W of 4 KiB: the rows
+    kernel hashes each block's W-byte window ending at the 16-B boundary
+    after the block, crc_window_fix_kernel trades the bytes where window and
+    block differ (front bytes of the window outside the block, a head of the
+    block before the window, the tail after the block).  Against the oracle
+    on every block, output pre-filled with a sentinel, at base offsets that
+    put the first block's window start before the base, at it and after it,
+    for 1, 2, 65 and 2049 blocks and a ~48 MiB batch; and against a context
+    with the window mode off."""
+    torch = torch_cuda
+    off_ctx = _ctx_env(PRISKV_CRC_WINDOW=0)
+    sentinel = int(np.int32(np.uint32(0xA5A5A5A5).view(np.int32)))
+    W = (bs + 15) // 4096 * 4096
+    for nb in sorted({1, 2, 65, 2049, (48 << 20) // bs + 3}):
+        t = _region(torch, ctx, bs * nb + 32, SEED ^ (bs * 5 + nb), nb)
+        for shift in (1, 3, 8, 13, 15) if bs % 1024 == 0 else (0, 1, 7, 12, 15):
+            view = t[shift:shift + bs * nb]
+            plan = ctx.blocks_plan(view.data_ptr(), nb, bs)
+            head = bs % 4 == 0 and (view.data_ptr() & 3) == 0 and 4 <= bs % 1024 <= 64
+            if not head:
+                assert plan.startswith("crc_rows_kernel<G=64,") and f"{W}-B windows" in plan, (bs, shift, plan)
+            want = O.crc32_blocks(view.cpu().numpy(), bs, nthreads=8)
+            for c in (ctx, off_ctx) if nb <= 2049 else (ctx,):
+                out = torch.full((nb,), sentinel, dtype=torch.int32, device="cuda")
+                c.blocks_dev(view, bs, out=out)
+                torch.cuda.synchronize()
+                got = _u32(out)
+                assert np.array_equal(got, want), (bs, nb, shift, plan, np.nonzero(got != want)[0][:8])
+        del t
+    off_ctx.close()
 
 
 @pytest.mark.slow

@@ -226,13 +226,24 @@ def test_path_selection():
     # any other size >= 16 B or base alignment: the uniform-stride kernel
     assert C.blocks_path(4096, 10, 100) == "stride"
     assert C.blocks_path(4097, 10, 100) == "stride"
-    assert C.blocks_path(4097, 10, 4096) == "stride"    # unaligned base
-    assert C.blocks_path(4104, 10, 4096) == "stride"    # 8-byte aligned only
+    # within W - 15 .. W + 48 B of a multiple W of 4 KiB up to 16 KiB (odd, or
+    # on an odd base): the rows kernel on 16-B aligned W-byte windows
+    assert C.blocks_path(4097, 10, 4096) == "window"    # unaligned base
+    assert C.blocks_path(4104, 10, 4096) == "window"    # 8-byte aligned only
+    assert C.blocks_path(4096, 10, 4081) == "window"
+    assert C.blocks_path(4096, 10, 4080) == "stride"
+    assert C.blocks_path(4096, 10, 4144) == "headsplit"   # the head split goes first
+    assert C.blocks_path(4097, 10, 4144) == "window"
+    assert C.blocks_path(4096, 10, 4145) == "stride"
+    assert C.blocks_path(4096, 10, 8191) == "window"
+    assert C.blocks_path(4096, 1 << 20, 16383) == "window"
+    assert C.blocks_path(4098, 10, 16432) == "window"
+    assert C.blocks_path(4096, 10, 20479) == "extents"   # beyond 16 KiB
     # whole KiB rows + a 4..64-B head (multiple of 4, 4-byte aligned base):
     # the rows kernel on the bodies + crc_head_kernel
     assert C.blocks_path(4096, 10, 4100) == "headsplit"
     assert C.blocks_path(4100, 10, 4100) == "headsplit"   # 4-byte aligned base
-    assert C.blocks_path(4098, 10, 4100) == "stride"      # 2-byte aligned base
+    assert C.blocks_path(4098, 10, 4100) == "window"      # 2-byte aligned base
     assert C.blocks_path(4096, 10, 1024 + 64) == "headsplit"
     assert C.blocks_path(4096, 10, 1024 + 68) == "stride"  # head above 64 B
     # few large head + body blocks: the rows kernel does not segment the
@@ -243,7 +254,8 @@ def test_path_selection():
     assert C.blocks_path(4096, 4096, (64 << 10) + 4) == "headsplit"   # 2 per wave: balanced
     assert C.blocks_path(4096, 1 << 16, (64 << 10) + 4) == "headsplit"
     assert C.blocks_path(4096, 10, (32 << 10) + 4) == "headsplit"      # bodies below 64 KiB
-    assert C.blocks_path(4096, 10, 4097) == "stride"      # odd
+    assert C.blocks_path(4096, 10, 4097) == "window"      # odd
+    assert C.blocks_path(4096, 10, 4200) == "stride"      # odd, beyond W + 48
     assert C.blocks_path(4096, 10, 1000) == "stride"
     assert C.blocks_path(4097, 10, 256) == "stride"     # sub-KiB power of two, unaligned base
     # the default limits hand larger stride sizes to the extents kernel

@@ -63,6 +63,11 @@ CASES = [("ranges 1x256MiB", 1, 256 << 20, 0), ("ranges 32x1MiB", 32, 1 << 20, (
          ("blocks odd4097", 1000000, 4097, 0), ("blocks odd4095", 1000000, 4095, 0),
          ("blocks odd1000", 4000000, 1000, 0), ("blocks odd2047", 2000000, 2047, 0),
          ("blocks odd8193", 500000, 8193, 0), ("blocks odd100", 40000000, 100, 0),
+         ("blocks odd8191", 500000, 8191, 0), ("blocks odd16383", 250000, 16383, 0),
+         ("blocks odd4111", 1000000, 4111, 0), ("blocks odd4200", 1000000, 4200, 0),
+         # (blocks: the 4th field is a base offset) 4 KiB blocks on an odd base
+         ("blocks base1 4096", 1000000, 4096, 1), ("blocks base8 4096", 1000000, 4096, 8),
+         ("small32 blocks 8192xodd4097", 8192, 4097, 0), ("small32 blocks 8192xodd4095", 8192, 4095, 0),
          # 32 MiB calls: few large values / blocks against the rows kernel
          ("small32 ranges 32x1MiB", 32, 1 << 20, 1 << 20), ("small32 ranges 16x2MiB", 16, 2 << 20, 2 << 20),
          ("small32 blocks 32x1MiB", 32, 1 << 20, 0), ("small32 blocks 8192x4KiB", 8192, 4096, 0),
@@ -114,7 +119,7 @@ for r in range(ROUNDS):
                     rc = L.priskv_crc32_ranges_dev(h, region.data_ptr(), offs.data_ptr(), lens.data_ptr(), n,
                                                    out.data_ptr(), sp)
                 else:
-                    rc = L.priskv_crc32_blocks_dev(h, region.data_ptr(), n, ln, out.data_ptr(), sp)
+                    rc = L.priskv_crc32_blocks_dev(h, region.data_ptr() + stride, n, ln, out.data_ptr(), sp)
                 assert rc == 0, rc
             for _ in range(20):
                 call()
