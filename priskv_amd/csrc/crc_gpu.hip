@@ -88,6 +88,7 @@ struct priskv_crc_ctx {
     uint32_t *d_sarwate;       // 256 words
     uint32_t *d_zpow;          // kZpowRows x 32 words: columns of Z_(2^k) (segment combine)
     uint32_t *d_rowshift;      // 16 x 4 x 32 words: columns of Z_-p o Z_(256(3-k)) (extents fold)
+    uint32_t *d_winimg;        // window mode images for W = 4, 8, 12, 16 KiB (crc_device.inc s_winimg)
     // host-streamed path (guarded by lock)
     pthread_mutex_t lock;
     int stream_ready;
@@ -1070,12 +1071,13 @@ int launch_head_split(const priskv_crc_ctx *ctx, const uint8_t *base, uint64_t n
 // KiB) that is odd or on an odd base -- 4095, 4097, 8193 B, 4096 B at base
 // + 1: the rows kernel hashes each block's window, the W bytes that end at
 // the first 16-B boundary at or after the block's end (crc_rows_kernel OPT
-// bit 13: aligned 1 KiB rows at W's plan, one chunk cursor jump per block),
-// and crc_window_fix_kernel trades the at most 15 + 63 bytes where window and
-// block differ.  The head split goes first (4-byte aligned
-// B = h + whole KiB rows).
-// PRISKV_CRC_WINDOW=0 turns it off (the stride kernel / extents path).
+// bit 13: aligned 1 KiB rows at W's plan), each CRC corrected for the bytes
+// where window and block differ when the wave stores 64 of them
+// (crc_device.inc s_winimg).  The head split goes first (4-byte aligned B = h +
+// whole KiB rows).  PRISKV_CRC_WINDOW=0 turns it off (the stride kernel /
+// extents path).
 constexpr uint32_t kWinMaxBytes = 16u << 10, kWinOver = 48;
+constexpr int kWinImages = (int)(kWinMaxBytes / 4096);
 constexpr int kWinOpt = 8192;
 
 uint32_t window_bytes(const priskv_crc_ctx *ctx, const void *base, uint64_t nblocks, uint32_t bs)
@@ -1115,7 +1117,7 @@ int launch_window(const priskv_crc_ctx *ctx, const uint8_t *base, uint64_t nbloc
     const uint64_t cps = W / ((uint64_t)P.CH * 16u * P.G);
     const uint32_t *img = ctx->d_lds_image[0];
     const uint32_t *fold = (P.opt & 32) ? ctx->d_nibrep[6] : ctx->d_fold + 6 * 2048;
-    const uint32_t *zp = ctx->d_zpow;
+    const uint32_t *zp = ctx->d_winimg + (W / 4096 - 1) * kWinImgWords; // (s_winimg)
     const uint64_t cap = max_wgs * NW * ((1ull << 31) / cps - 1);
     for (uint64_t done = 0; done < nblocks;) {
         uint64_t n = (nblocks - done < cap) ? nblocks - done : cap;
@@ -1132,13 +1134,7 @@ int launch_window(const priskv_crc_ctx *ctx, const uint8_t *base, uint64_t nbloc
             return rc;
         done += n;
     }
-    HeadCols z, z16;
-    prv_shift_columns(z.c, W);
-    prv_shift_columns(z16.c, W - 16);
-    const uint64_t want = (nblocks + 255) / 256;
-    const uint32_t grid = (uint32_t)(want < (uint64_t)ctx->num_cus * 8 ? want : (uint64_t)ctx->num_cus * 8);
-    return launch_k(crc_window_fix_kernel, dim3(grid), dim3(256), s, base, nblocks, bs, W, ctx->d_sarwate,
-                    ctx->d_rowshift, z, z16, out);
+    return 0;
 }
 
 // sub-KiB kernel for G = 1 << gl: no fold at G = 1 (a lane holds a whole
@@ -1455,7 +1451,7 @@ int priskv_crc32_blocks_plan(const priskv_crc_ctx *ctx, const void *d_base, uint
         const Plan &P = kPlans[p];
         w = snprintf(buf, len,
                      "crc_rows_kernel<G=%d,CH=%d,NBUF=%d,nt%s%s,progress-priority %d,window> (%u-B windows ending at "
-                     "the 16-B boundary after each block) + crc_window_fix_kernel",
+                     "the 16-B boundary after each block, head rows, masks, unshift)",
                      P.G, P.CH, P.NBUF, (P.opt & 2) ? ",pipelined-fold" : "", (P.opt & 32) ? ",nibble-fold" : "",
                      (P.opt >> 8) & 3, win);
     } else if (path == PATH_STRIDE) {
@@ -1648,6 +1644,23 @@ int priskv_crc_ctx_create(int device, priskv_crc_ctx **out)
     prv_rowshift_columns(h_img);
     if ((rc = herr(hipMemcpy(c->d_rowshift, h_img, sizeof(uint32_t) * 16 * 4 * 32, hipMemcpyHostToDevice))))
         goto fail;
+    static_assert(kWinImages * kWinImgWords <= PRV_LDS_WORDS, "window images fit the staging buffer");
+    for (int wi = 0; wi < kWinImages; wi++) {
+        uint32_t *im = h_img + wi * kWinImgWords;
+        const uint32_t W = 4096u * (uint32_t)(wi + 1);
+        prv_sarwate_table(im);
+        for (int k = 1; k < 4; k++)
+            for (int i = 0; i < 256; i++) {
+                const uint32_t v = im[(k - 1) * 256 + i];
+                im[k * 256 + i] = (v >> 8) ^ im[v & 0xff];
+            }
+        prv_shift_columns(im + 4 * 256, W);
+        prv_shift_columns(im + 4 * 256 + 32, W - 16);
+        prv_unshift_columns(im + 4 * 256 + 64);
+    }
+    if ((rc = herr(hipMalloc((void **)&c->d_winimg, sizeof(uint32_t) * kWinImages * kWinImgWords))) ||
+        (rc = herr(hipMemcpy(c->d_winimg, h_img, sizeof(uint32_t) * kWinImages * kWinImgWords, hipMemcpyHostToDevice))))
+        goto fail;
     for (int k = 0; k < kZpowRows; k++)
         prv_shift_columns(h_img + k * 32, 1ull << k);
     if ((rc = herr(hipMemcpy(c->d_zpow, h_img, sizeof(uint32_t) * kZpowRows * 32, hipMemcpyHostToDevice))))
@@ -1728,6 +1741,7 @@ void priskv_crc_ctx_destroy(priskv_crc_ctx *c)
     (void)hipFree(c->d_fold);
     (void)hipFree(c->d_sarwate);
     (void)hipFree(c->d_rowshift);
+    (void)hipFree(c->d_winimg);
     (void)hipFree(c->d_zpow);
     (void)hipFree(c->d_scrub);
     {

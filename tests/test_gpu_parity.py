@@ -1665,9 +1665,9 @@ _WINDOW_SIZES = [4081, 4095, 4096, 4097, 4099, 4111, 4112, 4127, 4144, 8177, 819
 def test_window_blocks(torch_cuda, ctx, bs):
     """Odd sizes (or 4 KiB on odd bases) near a multiple W of 4 KiB: the rows
     kernel hashes each block's W-byte window ending at the 16-B boundary
-    after the block, crc_window_fix_kernel trades the bytes where window and
-    block differ (front bytes of the window outside the block, a head of the
-    block before the window, the tail after the block).  Against the oracle
+    after the block, masking the window's bytes outside the block (front and
+    tail) and hashing the block's bytes before the window (head) as one more
+    row, then unshifts by the tail pad.  Against the oracle
     on every block, output pre-filled with a sentinel, at base offsets that
     put the first block's window start before the base, at it and after it,
     for 1, 2, 65 and 2049 blocks and a ~48 MiB batch; and against a context

@@ -67,6 +67,8 @@ CASES = [("ranges 1x256MiB", 1, 256 << 20, 0), ("ranges 32x1MiB", 32, 1 << 20, (
          ("blocks odd4111", 1000000, 4111, 0), ("blocks odd4200", 1000000, 4200, 0),
          # (blocks: the 4th field is a base offset) 4 KiB blocks on an odd base
          ("blocks base1 4096", 1000000, 4096, 1), ("blocks base8 4096", 1000000, 4096, 8),
+         ("blocks base0 4096", 1000000, 4096, 0), ("blocks base16 4096", 1000000, 4096, 16),
+         ("blocks base64 4096", 1000000, 4096, 64), ("blocks base128 4096", 1000000, 4096, 128),
          ("small32 blocks 8192xodd4097", 8192, 4097, 0), ("small32 blocks 8192xodd4095", 8192, 4095, 0),
          # 32 MiB calls: few large values / blocks against the rows kernel
          ("small32 ranges 32x1MiB", 32, 1 << 20, 1 << 20), ("small32 ranges 16x2MiB", 16, 2 << 20, 2 << 20),
