@@ -1654,9 +1654,20 @@ int priskv_crc_ctx_create(int device, priskv_crc_ctx **out)
                 const uint32_t v = im[(k - 1) * 256 + i];
                 im[k * 256 + i] = (v >> 8) ^ im[v & 0xff];
             }
-        prv_shift_columns(im + 4 * 256, W);
-        prv_shift_columns(im + 4 * 256 + 32, W - 16);
-        prv_unshift_columns(im + 4 * 256 + 64);
+        // nibble tables: Z_W, Z_(W - 16), Z_-p (p = 0..15)
+        uint32_t cols[18][32];
+        prv_shift_columns(cols[0], W);
+        prv_shift_columns(cols[1], W - 16);
+        prv_unshift_columns(&cols[2][0]);
+        for (int t = 0; t < 18; t++)
+            for (int nb = 0; nb < 8; nb++)
+                for (uint32_t v = 0; v < 16; v++) {
+                    uint32_t r = 0;
+                    for (int bit = 0; bit < 4; bit++)
+                        if ((v >> bit) & 1u)
+                            r ^= cols[t][4 * nb + bit];
+                    im[4 * 256 + t * kWinNib + nb * 16 + (int)v] = r;
+                }
     }
     if ((rc = herr(hipMalloc((void **)&c->d_winimg, sizeof(uint32_t) * kWinImages * kWinImgWords))) ||
         (rc = herr(hipMemcpy(c->d_winimg, h_img, sizeof(uint32_t) * kWinImages * kWinImgWords, hipMemcpyHostToDevice))))

@@ -1695,6 +1695,26 @@ def test_window_blocks(torch_cuda, ctx, bs):
     off_ctx.close()
 
 
+@pytest.mark.parametrize("bs,shift", [(4095, 3), (4097, 0), (4111, 9)])
+def test_window_blocks_deep_plan(torch_cuda, ctx, bs, shift):
+    """Window mode on the deep 4 KiB plan (batches of >= 2^18 blocks: four
+    chunks in flight): 2^18 + 77 blocks (~1 GiB), every CRC against the
+    oracle -- every wave's range ends in a partial group of 64 and starts
+    from a carried granule loaded before its loop."""
+    torch = torch_cuda
+    nb = (1 << 18) + 77
+    t = _region(torch, ctx, bs * nb + 32, SEED ^ (bs * 7 + shift), 3)
+    view = t[shift:shift + bs * nb]
+    plan = ctx.blocks_plan(view.data_ptr(), nb, bs)
+    assert plan.startswith("crc_rows_kernel<G=64,CH=4,NBUF=4,") and "4096-B windows" in plan, plan
+    got = _u32(ctx.blocks_dev(view, bs, nblocks=nb))
+    torch.cuda.synchronize()
+    want = O.crc32_blocks(view.cpu().numpy(), bs, nthreads=16)
+    assert np.array_equal(got, want), (bs, shift, np.nonzero(got != want)[0][:8])
+    del t, view
+    torch.cuda.empty_cache()
+
+
 @pytest.mark.slow
 def test_stride_kernel_beyond_4GiB(torch_cuda, ctx):
     """1.1 M blocks of 4100 B (4.5 GB, group pointers past 2^32) on an
