@@ -1451,7 +1451,7 @@ int priskv_crc32_blocks_plan(const priskv_crc_ctx *ctx, const void *d_base, uint
         const Plan &P = kPlans[p];
         w = snprintf(buf, len,
                      "crc_rows_kernel<G=%d,CH=%d,NBUF=%d,nt%s%s,progress-priority %d,window> (%u-B windows ending at "
-                     "the 16-B boundary after each block, head rows, masks, unshift)",
+                     "the 16-B boundary after each block, corrected as each 64 CRCs are stored)",
                      P.G, P.CH, P.NBUF, (P.opt & 2) ? ",pipelined-fold" : "", (P.opt & 32) ? ",nibble-fold" : "",
                      (P.opt >> 8) & 3, win);
     } else if (path == PATH_STRIDE) {

@@ -1315,11 +1315,17 @@ def test_blocks_plan_strings(torch_cuda, ctx):
     # ... else segments + combine
     assert "crc_combine_segments_kernel" in ctx.blocks_plan(base, 1000, (1 << 20) + 2048)
     assert ctx.blocks_plan(base, 100, 256) == "crc_small_kernel<G=16,byte-fold>"
-    # odd sizes and unaligned bases: the uniform-stride kernel
-    assert ctx.blocks_plan(base + 1, 100, 4096).startswith("crc_stride_kernel<G=32,CH=8,NBUF=2,nt,progress-priority 3> (8 rows of 512 B")
-    assert ctx.blocks_plan(base + 1, 100, 4100).startswith("crc_stride_kernel<G=32,CH=8,NBUF=2,nt,progress-priority 3> "
+    # odd sizes or bases near a multiple of 4 KiB: the rows kernel on windows
+    for bs, mis in ((4096, 1), (4100, 1), (4095, 0), (4097, 8)):
+        assert ctx.blocks_plan(base + mis, 100, bs) == (
+            "crc_rows_kernel<G=64,CH=4,NBUF=3,nt,pipelined-fold,nibble-fold,progress-priority 3,window> (4096-B "
+            "windows ending at the 16-B boundary after each block, corrected as each 64 CRCs are stored)"), (bs, mis)
+    assert ctx.blocks_plan(base + 1, 100, 8193).startswith("crc_rows_kernel<G=64,CH=4,NBUF=2,nt,nibble-fold,"
+                                                           "progress-priority 1,window> (8192-B windows")
+    # other odd sizes and unaligned bases: the uniform-stride kernel
+    assert ctx.blocks_plan(base + 1, 100, 4200).startswith("crc_stride_kernel<G=32,CH=8,NBUF=2,nt,progress-priority 3> "
                                                            "(9 rows of 512 B "
-                                                           "per block, 508 B in front)")
+                                                           "per block, 408 B in front)")
     # whole KiB rows + a 4-64 B head on a 4-byte aligned base: rows kernel + head terms
     assert ctx.blocks_plan(base, 100, 4100) == ("crc_rows_kernel<G=64,CH=4,NBUF=3,nt,pipelined-fold,nibble-fold,"
                                                 "progress-priority 3> on the 4096-B bodies + crc_head_kernel "
