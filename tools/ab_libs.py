@@ -65,6 +65,9 @@ CASES = [("ranges 1x256MiB", 1, 256 << 20, 0), ("ranges 32x1MiB", 32, 1 << 20, (
          ("blocks odd8193", 500000, 8193, 0), ("blocks odd100", 40000000, 100, 0),
          ("blocks odd8191", 500000, 8191, 0), ("blocks odd16383", 250000, 16383, 0),
          ("blocks odd4111", 1000000, 4111, 0), ("blocks odd4200", 1000000, 4200, 0),
+         ("blocks odd2049", 2000000, 2049, 0), ("blocks odd3071", 1300000, 3071, 0),
+         ("blocks odd3073", 1300000, 3073, 0), ("blocks odd5121", 800000, 5121, 0),
+         ("blocks odd6143", 650000, 6143, 0), ("blocks odd10239", 400000, 10239, 0),
          # (blocks: the 4th field is a base offset) 4 KiB blocks on an odd base
          ("blocks base1 4096", 1000000, 4096, 1), ("blocks base8 4096", 1000000, 4096, 8),
          ("blocks base0 4096", 1000000, 4096, 0), ("blocks base16 4096", 1000000, 4096, 16),
