@@ -1077,54 +1077,76 @@ int launch_head_split(const priskv_crc_ctx *ctx, const uint8_t *base, uint64_t n
 // whole KiB rows).  PRISKV_CRC_WINDOW=0 turns it off (the stride kernel /
 // extents path).
 constexpr uint32_t kWinMaxBytes = 16u << 10, kWinOver = 48;
-constexpr int kWinImages = (int)(kWinMaxBytes / 4096);
+constexpr uint32_t kStrideMax = 9u << 10; // the stride / extents kernels' boundary (stride_to_extents)
+constexpr int kWinImages = (int)(kWinMaxBytes / 1024);
 constexpr int kWinOpt = 8192;
 
 uint32_t window_bytes(const priskv_crc_ctx *ctx, const void *base, uint64_t nblocks, uint32_t bs)
 {
-    const uint32_t W = (uint32_t)(((uint64_t)bs + 15) / 4096 * 4096); // W - 15 <= bs
+    const uint32_t W = (uint32_t)(((uint64_t)bs + 15) / 1024 * 1024); // W - 15 <= bs
     (void)base;
     (void)nblocks; // (blocks this small are never segmented: kSegMinLen)
     static_assert(kWinMaxBytes + kWinOver < kSegMinLen, "window sizes are never segmented");
-    return ((ctx && !ctx->window) || W == 0 || W > kWinMaxBytes || bs > W + kWinOver) ? 0u : W;
+    if ((ctx && !ctx->window) || W == 0 || W > kWinMaxBytes || bs > W + kWinOver)
+        return 0;
+    // W not a multiple of 4 KiB (the G = 16 plans): only below 9 KiB, and
+    // there only where the stride kernel pads a whole extra row (B > W), or
+    // for W = 1 KiB below it.  Per ~4 GB call (profiles/r05/window/g16_*):
+    // 1025 B 843 -> 693 us, 2049 B 791 -> 687, 3073 B 673 -> 656, 1023 B
+    // 713 -> 682; but 2047 / 3071 / 6143 B level or slower, 2048 B on base
+    // + 1 643 -> 676, and from 9 KiB the extents kernel is faster (9217 B
+    // 644 against 649, 15361 B 602 against 633, 10239 B 639 against 667)
+    if (W % 4096 != 0 && (W >= kStrideMax || (W > 1024 && bs <= W) || (W == 1024 && bs == W)))
+        return 0;
+    return W;
 }
 
 template <int P>
 const void *window_kernel_p()
 {
     constexpr Plan Q = kPlans[P];
-    static_assert(Q.G == 64, "window mode: one block per wave group");
+    static_assert(!(Q.opt & 1024), "window mode: 8-wave workgroups");
     return plan_kernel<Q.G, Q.CH, Q.NBUF, Q.opt | kWinOpt>();
 }
 
+// the window kernel of W's plan: G = 64 for multiples of 4 KiB, G = 16 (four
+// blocks per wave group) for the other whole KiB multiples
 const void *window_fn(int p)
 {
     switch (p) {
     case PLAN_4K: return window_kernel_p<PLAN_4K>();
     case PLAN_4K_DEEP: return window_kernel_p<PLAN_4K_DEEP>();
     case PLAN_G64_CH4_NIB: return window_kernel_p<PLAN_G64_CH4_NIB>();
+    case PLAN_G16_CH4: return window_kernel_p<PLAN_G16_CH4>();
+    case PLAN_G16_CH4_PIPE: return window_kernel_p<PLAN_G16_CH4_PIPE>();
     default: return window_kernel_p<PLAN_G64_CH4>();
     }
 }
 
+int launch_stride(const priskv_crc_ctx *ctx, const uint8_t *base, uint64_t nblocks, uint32_t bs, uint32_t *out,
+                  hipStream_t s);
+
 int launch_window(const priskv_crc_ctx *ctx, const uint8_t *base, uint64_t nblocks, uint32_t bs, uint32_t W,
                   uint32_t *out, hipStream_t s)
 {
-    const int p = plan_for(W, nblocks); // 4 KiB, 4 KiB deep, 8 KiB or the G64 CH4 plan
+    const int p = plan_for(W, nblocks);
     const Plan &P = kPlans[p];
+    const uint64_t per = 64 / (uint64_t)P.G; // blocks per wave group
+    const int gi = P.G == 64 ? 0 : (P.G == 32 ? 1 : 2);
     const uint64_t max_wgs = (uint64_t)ctx->num_cus * ctx->plan_wgs_per_cu[p];
     const uint64_t NW = (uint64_t)plan_waves(p);
     const uint64_t cps = W / ((uint64_t)P.CH * 16u * P.G);
-    const uint32_t *img = ctx->d_lds_image[0];
-    const uint32_t *fold = (P.opt & 32) ? ctx->d_nibrep[6] : ctx->d_fold + 6 * 2048;
-    const uint32_t *zp = ctx->d_winimg + (W / 4096 - 1) * kWinImgWords; // (s_winimg)
+    const uint32_t *img = ctx->d_lds_image[gi];
+    const uint32_t *fold = (P.opt & 32) ? ctx->d_nibrep[log2u(P.G)] : ctx->d_fold + log2u(P.G) * 2048;
+    const uint32_t *zp = ctx->d_winimg + (W / 1024 - 1) * kWinImgWords; // (s_winimg)
     const uint64_t cap = max_wgs * NW * ((1ull << 31) / cps - 1);
-    for (uint64_t done = 0; done < nblocks;) {
-        uint64_t n = (nblocks - done < cap) ? nblocks - done : cap;
+    const uint64_t ngroups = nblocks / per;
+    for (uint64_t done = 0; done < ngroups;) {
+        uint64_t n = (ngroups - done < cap) ? ngroups - done : cap;
         const uint64_t want = (n + NW - 1) / NW;
         const uint32_t grid = (uint32_t)(want < max_wgs ? want : max_wgs);
-        const uint8_t *b = base + done * bs;
-        uint32_t *o = out + done;
+        const uint8_t *b = base + done * per * bs;
+        uint32_t *o = out + done * per;
         uint32_t xw = n >= 32ull * grid * NW ? ctx->plan_xw[p] : 0u, tile = 0, one = 1, stride = bs, wb = W;
         uint32_t *none = nullptr;
         void *args[] = {(void *)&b,  (void *)&n,    (void *)&wb,   (void *)&img,    (void *)&fold,
@@ -1134,7 +1156,14 @@ int launch_window(const priskv_crc_ctx *ctx, const uint8_t *base, uint64_t nbloc
             return rc;
         done += n;
     }
-    return 0;
+    // a ragged tail of fewer than a group's blocks (G = 16): the stride kernel
+    // or, from 9 KiB, the extents kernel
+    const uint64_t head = ngroups * per;
+    if (head == nblocks)
+        return 0;
+    if (bs >= kStrideMax)
+        return launch_extents(ctx, base + head * bs, nblocks - head, nullptr, nullptr, bs, bs, out + head, s);
+    return launch_stride(ctx, base + head * bs, nblocks - head, bs, out + head, s);
 }
 
 // sub-KiB kernel for G = 1 << gl: no fold at G = 1 (a lane holds a whole
@@ -1198,8 +1227,6 @@ struct StridePlan {
 // odd sizes up to 8.5 KiB (4609 B 5.84 / 5.19 extents, 8193 B 6.10 / 5.70,
 // 8705 B 6.01 / 5.88) and trails from 9 KiB (9217 B 6.04 / 6.11, 10 241 B
 // 6.01 / 6.37; profiles/r03/stride_prio/).
-constexpr uint32_t kStrideMax = 9u << 10;
-
 bool stride_to_extents(const void *base, uint32_t bs)
 {
     (void)base;
@@ -1644,10 +1671,12 @@ int priskv_crc_ctx_create(int device, priskv_crc_ctx **out)
     prv_rowshift_columns(h_img);
     if ((rc = herr(hipMemcpy(c->d_rowshift, h_img, sizeof(uint32_t) * 16 * 4 * 32, hipMemcpyHostToDevice))))
         goto fail;
-    static_assert(kWinImages * kWinImgWords <= PRV_LDS_WORDS, "window images fit the staging buffer");
+    if ((rc = herr(hipMalloc((void **)&c->d_winimg, sizeof(uint32_t) * kWinImages * kWinImgWords))))
+        goto fail;
+    static_assert(kWinImgWords <= PRV_LDS_WORDS, "a window image fits the staging buffer");
     for (int wi = 0; wi < kWinImages; wi++) {
-        uint32_t *im = h_img + wi * kWinImgWords;
-        const uint32_t W = 4096u * (uint32_t)(wi + 1);
+        uint32_t *im = h_img;
+        const uint32_t W = 1024u * (uint32_t)(wi + 1);
         prv_sarwate_table(im);
         for (int k = 1; k < 4; k++)
             for (int i = 0; i < 256; i++) {
@@ -1668,10 +1697,10 @@ int priskv_crc_ctx_create(int device, priskv_crc_ctx **out)
                             r ^= cols[t][4 * nb + bit];
                     im[4 * 256 + t * kWinNib + nb * 16 + (int)v] = r;
                 }
+        if ((rc = herr(hipMemcpy(c->d_winimg + wi * kWinImgWords, h_img, sizeof(uint32_t) * kWinImgWords,
+                                 hipMemcpyHostToDevice))))
+            goto fail;
     }
-    if ((rc = herr(hipMalloc((void **)&c->d_winimg, sizeof(uint32_t) * kWinImages * kWinImgWords))) ||
-        (rc = herr(hipMemcpy(c->d_winimg, h_img, sizeof(uint32_t) * kWinImages * kWinImgWords, hipMemcpyHostToDevice))))
-        goto fail;
     for (int k = 0; k < kZpowRows; k++)
         prv_shift_columns(h_img + k * 32, 1ull << k);
     if ((rc = herr(hipMemcpy(c->d_zpow, h_img, sizeof(uint32_t) * kZpowRows * 32, hipMemcpyHostToDevice))))

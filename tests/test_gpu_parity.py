@@ -1334,9 +1334,15 @@ def test_blocks_plan_strings(torch_cuda, ctx):
     assert ctx.blocks_plan(base, 100, 100).startswith("crc_stride_kernel<G=8,CH=8,NBUF=2,nt,byte-fold,progress-priority 3> (1 rows of 128 B")
     # the extents kernel from 9 KiB, odd sizes and multiples of 4 alike
     assert ctx.blocks_plan(base, 100, 4609).startswith("crc_stride_kernel<G=32,CH=8,NBUF=2,nt,progress-priority 3>")
-    assert ctx.blocks_plan(base, 100, 9215).startswith("crc_stride_kernel<")
+    assert ctx.blocks_plan(base, 100, 9100).startswith("crc_stride_kernel<")
     assert ctx.blocks_plan(base, 100, 9217) == "crc_ranges_kernel (extents)"
+    assert ctx.blocks_plan(base, 100, 2049).startswith("crc_rows_kernel<G=16,CH=4,NBUF=2,nt,progress-priority 1,"
+                                                      "window> (2048-B windows")
+    assert ctx.blocks_plan(base, 100, 1025).startswith("crc_rows_kernel<G=16,CH=4,NBUF=2,nt,pipelined-fold,"
+                                                      "nibble-fold,progress-priority 1,window> (1024-B windows")
+    assert ctx.blocks_plan(base, 100, 9281) == "crc_ranges_kernel (extents)"
     assert ctx.blocks_plan(base, 100, 9212).startswith("crc_stride_kernel<G=32,CH=8,NBUF=2,nt,progress-priority 3> (18 rows of 512 B")
+    assert ctx.blocks_plan(base, 100, 8700).startswith("crc_stride_kernel<G=32,CH=8,NBUF=2,nt,progress-priority 3> (17 rows of 512 B")
     assert ctx.blocks_plan(base, 100, 9300) == "crc_ranges_kernel (extents)"
     assert "crc_head_kernel (4-B heads)" in ctx.blocks_plan(base, 100, 9220)
     assert ctx.blocks_plan(base, 100, 15) == "crc_generic_kernel"
@@ -1611,7 +1617,7 @@ def test_fused_single_value_beyond_2GiB(torch_cuda, ctx, kind):
 # (G, block sizes whose cost-model plan is G lanes per block): G < 16 only
 # with one row per block; G = 64 never wins below the 9 KiB limit
 _STRIDE_SIZES = {2: [16, 17, 23, 32], 4: [33, 48, 50, 64], 8: [65, 100, 127, 128],
-                 16: [129, 255, 257, 520, 700], 32: [769, 1000, 1023, 4200, 8301, 9215]}
+                 16: [129, 255, 257, 520, 700], 32: [769, 1000, 1006, 4200, 8301, 9100]}
 
 
 @pytest.mark.parametrize("G", sorted(_STRIDE_SIZES))
@@ -1664,7 +1670,10 @@ def test_stride_kernel_cost_model_sizes(torch_cuda, ctx, misalign):
 
 # block sizes within W - 15 .. W + 48 B of W = 4, 8, 12, 16 KiB: window mode
 _WINDOW_SIZES = [4081, 4095, 4096, 4097, 4099, 4111, 4112, 4127, 4144, 8177, 8191, 8193, 8240, 12287, 12300,
-                 16369, 16383, 16385, 16432]
+                 16369, 16383, 16385, 16432,
+                 # other whole-KiB W below 9 KiB (G = 16: four blocks per wave group),
+                 # B > W or W = 1 KiB
+                 1009, 1023, 1025, 1071, 1072, 2049, 3073, 6145, 7169, 8239]
 
 
 @pytest.mark.parametrize("bs", _WINDOW_SIZES)
@@ -1681,7 +1690,8 @@ def test_window_blocks(torch_cuda, ctx, bs):
     torch = torch_cuda
     off_ctx = _ctx_env(PRISKV_CRC_WINDOW=0)
     sentinel = int(np.int32(np.uint32(0xA5A5A5A5).view(np.int32)))
-    W = (bs + 15) // 4096 * 4096
+    W = (bs + 15) // 1024 * 1024
+    G = 64 if W % 4096 == 0 else 16
     for nb in sorted({1, 2, 65, 2049, (48 << 20) // bs + 3}):
         t = _region(torch, ctx, bs * nb + 32, SEED ^ (bs * 5 + nb), nb)
         for shift in (1, 3, 8, 13, 15) if bs % 1024 == 0 else (0, 1, 7, 12, 15):
@@ -1689,7 +1699,7 @@ def test_window_blocks(torch_cuda, ctx, bs):
             plan = ctx.blocks_plan(view.data_ptr(), nb, bs)
             head = bs % 4 == 0 and (view.data_ptr() & 3) == 0 and 4 <= bs % 1024 <= 64
             if not head:
-                assert plan.startswith("crc_rows_kernel<G=64,") and f"{W}-B windows" in plan, (bs, shift, plan)
+                assert plan.startswith(f"crc_rows_kernel<G={G},") and f"{W}-B windows" in plan, (bs, shift, plan)
             want = O.crc32_blocks(view.cpu().numpy(), bs, nthreads=8)
             for c in (ctx, off_ctx) if nb <= 2049 else (ctx,):
                 out = torch.full((nb,), sentinel, dtype=torch.int32, device="cuda")
@@ -1752,6 +1762,7 @@ def test_stride_kernel_beyond_4GiB(torch_cuda, ctx):
                                                (4607, 6000, 1, "crc_stride_kernel<G=32,", False),
                                                (4609, 6000, 0, "crc_stride_kernel<G=32,", False),
                                                (9217, 3000, 0, "crc_ranges_kernel (extents)", False),
+                                               (9400, 3000, 0, "crc_ranges_kernel (extents)", False),
                                                (16460, 3000, 0, "crc_ranges_kernel (extents)", False),
                                                (16388, 3000, 0, "crc_rows_kernel<G=64,", False),
                                                (4100, 2049, 4, "crc_rows_kernel<G=64,", False)])

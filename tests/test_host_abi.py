@@ -239,6 +239,15 @@ def test_path_selection():
     assert C.blocks_path(4096, 1 << 20, 16383) == "window"
     assert C.blocks_path(4098, 10, 16432) == "window"
     assert C.blocks_path(4096, 10, 20479) == "extents"   # beyond 16 KiB
+    # other whole-KiB multiples W >= 1 KiB (four blocks per wave group)
+    assert C.blocks_path(4096, 10, 1023) == "window"
+    assert C.blocks_path(4096, 10, 1071) == "window"
+    assert C.blocks_path(4096, 10, 1072) == "headsplit"    # the head split goes first
+    assert C.blocks_path(4096, 10, 1073) == "stride"
+    assert C.blocks_path(4096, 10, 1008) == "stride"
+    assert C.blocks_path(4096, 10, 2049) == "window"
+    assert C.blocks_path(4096, 10, 2047) == "stride"      # just below W (not 4 KiB): the stride kernel
+    assert C.blocks_path(4096, 10, 9215) == "stride"
     # whole KiB rows + a 4..64-B head (multiple of 4, 4-byte aligned base):
     # the rows kernel on the bodies + crc_head_kernel
     assert C.blocks_path(4096, 10, 4100) == "headsplit"
@@ -261,9 +270,15 @@ def test_path_selection():
     # the default limits hand larger stride sizes to the extents kernel
     assert C.blocks_path(4096, 10, 4607) == "stride"
     assert C.blocks_path(4096, 10, 4609) == "stride"
-    assert C.blocks_path(4096, 10, 9217) == "extents"   # odd from 9 KiB
-    assert C.blocks_path(4097, 10, 9216) == "extents"   # unaligned base counts as odd
+    assert C.blocks_path(4096, 10, 9217) == "extents"   # G = 16 windows stop below 9 KiB
+    assert C.blocks_path(4097, 10, 9216) == "extents"   # 9 KiB on an odd base
+    assert C.blocks_path(4097, 10, 2048) == "stride"    # B = W (not 4 KiB) on an odd base
+    assert C.blocks_path(4097, 10, 8192) == "window"    # ... a 4 KiB multiple does window
+    assert C.blocks_path(4096, 10, 7169) == "window"
+    assert C.blocks_path(4096, 10, 9300) == "extents"   # odd from 9 KiB
+    assert C.blocks_path(4097, 10, 9300) == "extents"   # unaligned base counts as odd
     assert C.blocks_path(4096, 10, 9212) == "stride"
+    assert C.blocks_path(4096, 10, 8700) == "stride"
     assert C.blocks_path(4096, 10, 9300) == "extents"   # multiples of 4 from 9 KiB (head 84 B)
     assert C.blocks_path(4096, 10, (64 << 20) + 5) == "extents"
     assert C.blocks_path(4096, 10, 15) == "generic"     # below one 16-B window

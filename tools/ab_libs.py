@@ -68,6 +68,11 @@ CASES = [("ranges 1x256MiB", 1, 256 << 20, 0), ("ranges 32x1MiB", 32, 1 << 20, (
          ("blocks odd2049", 2000000, 2049, 0), ("blocks odd3071", 1300000, 3071, 0),
          ("blocks odd3073", 1300000, 3073, 0), ("blocks odd5121", 800000, 5121, 0),
          ("blocks odd6143", 650000, 6143, 0), ("blocks odd10239", 400000, 10239, 0),
+         ("blocks odd1023", 4000000, 1023, 0), ("blocks odd1025", 4000000, 1025, 0),
+         ("blocks odd9217", 435000, 9217, 0), ("blocks odd15361", 260000, 15361, 0),
+         ("blocks base1 2048", 2000000, 2048, 1),
+         ("blocks al1024", 4000000, 1024, 0), ("blocks al2048", 2000000, 2048, 0),
+         ("blocks al3072", 1300000, 3072, 0), ("blocks al6144", 650000, 6144, 0),
          # (blocks: the 4th field is a base offset) 4 KiB blocks on an odd base
          ("blocks base1 4096", 1000000, 4096, 1), ("blocks base8 4096", 1000000, 4096, 8),
          ("blocks base0 4096", 1000000, 4096, 0), ("blocks base16 4096", 1000000, 4096, 16),
