@@ -1126,6 +1126,16 @@ const void *window_fn(int p)
 int launch_stride(const priskv_crc_ctx *ctx, const uint8_t *base, uint64_t nblocks, uint32_t bs, uint32_t *out,
                   hipStream_t s);
 
+// the XCD weights of a window launch over nblocks (one launch: from 32
+// groups per resident wave, as launch_plan applies them)
+uint32_t window_xw(const priskv_crc_ctx *ctx, int p, uint64_t nblocks)
+{
+    const uint64_t n = nblocks / (64 / (uint64_t)kPlans[p].G), NW = (uint64_t)plan_waves(p);
+    const uint64_t max_wgs = (uint64_t)ctx->num_cus * ctx->plan_wgs_per_cu[p];
+    const uint64_t want = (n + NW - 1) / NW, grid = want < max_wgs ? want : max_wgs;
+    return n >= 32ull * grid * NW ? ctx->plan_xw[p] : 0u;
+}
+
 int launch_window(const priskv_crc_ctx *ctx, const uint8_t *base, uint64_t nblocks, uint32_t bs, uint32_t W,
                   uint32_t *out, hipStream_t s)
 {
@@ -1476,11 +1486,15 @@ int priskv_crc32_blocks_plan(const priskv_crc_ctx *ctx, const void *d_base, uint
     if (win) {
         const int p = plan_for(win, nblocks);
         const Plan &P = kPlans[p];
+        const uint32_t xw = window_xw(ctx, p, nblocks);
+        char xs[32] = "";
+        if (xw)
+            snprintf(xs, sizeof(xs), ",xcd-weighted %u:%u", xw >> 16, xw & 0xFFFF);
         w = snprintf(buf, len,
-                     "crc_rows_kernel<G=%d,CH=%d,NBUF=%d,nt%s%s,progress-priority %d,window> (%u-B windows ending at "
-                     "the 16-B boundary after each block, corrected as each 64 CRCs are stored)",
+                     "crc_rows_kernel<G=%d,CH=%d,NBUF=%d,nt%s%s,progress-priority %d,window%s> (%u-B windows ending "
+                     "at the 16-B boundary after each block, corrected as each 64 CRCs are stored)",
                      P.G, P.CH, P.NBUF, (P.opt & 2) ? ",pipelined-fold" : "", (P.opt & 32) ? ",nibble-fold" : "",
-                     (P.opt >> 8) & 3, win);
+                     (P.opt >> 8) & 3, xs, win);
     } else if (path == PATH_STRIDE) {
         const StridePlan P = stride_plan(block_size);
         if (stride_to_extents(d_base, block_size)) {

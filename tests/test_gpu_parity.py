@@ -1711,18 +1711,24 @@ def test_window_blocks(torch_cuda, ctx, bs):
     off_ctx.close()
 
 
-@pytest.mark.parametrize("bs,shift", [(4095, 3), (4097, 0), (4111, 9)])
-def test_window_blocks_deep_plan(torch_cuda, ctx, bs, shift):
-    """Window mode on the deep 4 KiB plan (batches of >= 2^18 blocks: four
-    chunks in flight): 2^18 + 77 blocks (~1 GiB), every CRC against the
-    oracle -- every wave's range ends in a partial group of 64 and starts
-    from a carried granule loaded before its loop."""
+@pytest.mark.parametrize("bs,shift,nb,kernel", [(4095, 3, (1 << 18) + 77, "crc_rows_kernel<G=64,CH=4,NBUF=4,"),
+                                                (4097, 0, (1 << 18) + 77, "crc_rows_kernel<G=64,CH=4,NBUF=4,"),
+                                                (4111, 9, (1 << 18) + 77, "crc_rows_kernel<G=64,CH=4,NBUF=4,"),
+                                                (1025, 5, (1 << 18) + 78, "crc_rows_kernel<G=16,CH=4,NBUF=2,nt,pipelined"),
+                                                (2049, 0, 300003, "crc_rows_kernel<G=16,CH=4,NBUF=2,nt,progress")])
+def test_window_blocks_deep_plan(torch_cuda, ctx, bs, shift, nb, kernel):
+    """Window mode on large batches: the deep 4 KiB plan (>= 2^18 blocks:
+    four chunks in flight), and the G = 16 plans with >= 32 groups per
+    resident wave, where the XCD weights split the groups; every CRC against
+    the oracle -- every wave's range ends in a partial group of 64 blocks
+    and starts from a carried granule loaded before its loop, and a ragged
+    tail of < 4 blocks (G = 16) goes to the stride kernel."""
     torch = torch_cuda
-    nb = (1 << 18) + 77
     t = _region(torch, ctx, bs * nb + 32, SEED ^ (bs * 7 + shift), 3)
     view = t[shift:shift + bs * nb]
     plan = ctx.blocks_plan(view.data_ptr(), nb, bs)
-    assert plan.startswith("crc_rows_kernel<G=64,CH=4,NBUF=4,") and "4096-B windows" in plan, plan
+    W = (bs + 15) // 1024 * 1024
+    assert plan.startswith(kernel) and f"{W}-B windows" in plan and ",window,xcd-weighted 31:29>" in plan, plan
     got = _u32(ctx.blocks_dev(view, bs, nblocks=nb))
     torch.cuda.synchronize()
     want = O.crc32_blocks(view.cpu().numpy(), bs, nthreads=16)
