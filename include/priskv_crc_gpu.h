@@ -197,14 +197,17 @@ int priskv_crc_fill_splitmix_dev(const priskv_crc_ctx *ctx, void *d_dst, uint64_
  * blocks (16-byte aligned base), 5 = uniform stride (any other block of
  * 16 B up to 9 KiB: rows aligned to each block's end), 2 = extents (the
  * larger such blocks), 4 = generic (blocks
- * below 16 B: one thread per block), 6 = head split (a multiple of 4 that is
- * whole KiB rows plus a 4-64 B head, 4-byte aligned base: the rows kernel on
+ * below 16 B: one thread per block), 7 = window (a block not a multiple
+ * of 1 KiB on a 16-B aligned base, within W - 15 .. W + 48 B of a multiple
+ * W of 4 KiB up to 16 KiB -- 4095, 4097, 4100, 8193 B, 4096 B on an odd
+ * base -- or up to 48 B above another whole-KiB W below 9 KiB -- 1025,
+ * 2049 B: the rows kernel on each block's 16-B aligned W-byte window, then
+ * the few bytes where window and block differ), 6 = head split (a multiple
+ * of 4 that is whole 4 KiB chunks of at least 12 KiB plus a 4-64 B head on
+ * a 4-byte aligned base, that the window does not take: the rows kernel on
  * the bodies, then the heads' terms; not for a batch of few blocks with
  * bodies of 64 KiB and more, which the extents path segments -- judged for a
- * 256-CU device), 7 = window (any other block within W - 15 .. W + 48 B
- * of a multiple W of 4 KiB up to 16 KiB -- 4095, 4097, 8193 B, 4096 B on an
- * odd base: the rows kernel on each block's 16-B aligned W-byte window, then
- * the few bytes where window and block differ).  The exact kernels a given context launches, few-block
+ * 256-CU device).  The exact kernels a given context launches, few-block
  * segmentation included, are reported by
  * priskv_crc32_blocks_plan.  For tests and benchmarks; -EINVAL for invalid
  * arguments. */

@@ -1039,14 +1039,22 @@ int launch_rows_plain(const priskv_crc_ctx *ctx, const uint8_t *base, uint64_t n
 // balanced over the rows kernel's waves -- keeps the stride / extents paths,
 // which hand it to the fused kernel (whatever the body: 1023 KiB bodies cannot
 // be halved into whole-KiB segments, and one wave streams ~3.4 GB/s).
+// Round 5: the window mode takes heads of up to 48 B below 16 KiB first, and
+// the head split now runs only on bodies that are whole 4 KiB chunks of at
+// least 12 KiB -- against the stride / extents kernels (same process, ~4 GB
+// per call, profiles/r05/window/headsplit_*.jsonl) it gained 16436 B +4-7 %,
+// 1 MiB + 4 +6-7 %, 64 KiB + 4 +2-3 %, 12340 B +2 %, but lost 1088 B -19 %,
+// 17412 B -22 % (1 KiB and 17 KiB bodies: the G16 and one-row plans), 8244
+// B -4-6 % and 4148 / 9220 B -2 %.
 // PRISKV_CRC_HEADSPLIT=0 turns it off.  ctx = nullptr: a default context on
 // a device of kNominalCus CUs (priskv_crc32_blocks_path).
 constexpr int kNominalCus = 256; // MI355X
+constexpr uint32_t kHeadMinBody = 12u << 10;
 bool head_split(const priskv_crc_ctx *ctx, const void *base, uint64_t nblocks, uint32_t bs)
 {
     const uint32_t h = bs % PRV_ROW_BYTES, body = bs - h;
     if (!((!ctx || ctx->head_split) && bs % 4 == 0 && ((uintptr_t)base & 3) == 0 && h >= 4 && h <= kHeadMax &&
-          body >= PRV_ROW_BYTES))
+          body >= kHeadMinBody && body % 4096 == 0))
         return false;
     const bool seg = ctx ? ctx->segment != 0 : true;
     const uint64_t waves = (uint64_t)(ctx ? ctx->num_cus : kNominalCus) * kWaves;
@@ -1067,14 +1075,16 @@ int launch_head_split(const priskv_crc_ctx *ctx, const uint8_t *base, uint64_t n
 }
 
 // ---- window blocks -------------------------------------------------------------
-// A block size B within [W - 15, W + 48] of a multiple W of 4 KiB (W <= 16
-// KiB) that is odd or on an odd base -- 4095, 4097, 8193 B, 4096 B at base
-// + 1: the rows kernel hashes each block's window, the W bytes that end at
+// A block size B within [W - 15, W + 48] of a whole number W of KiB (W <= 16
+// KiB; window_bytes says which) that is not a multiple of 1 KiB on a 16-B
+// aligned base -- 4095, 4097, 8193, 1025, 2049 B, 4100 B, 4096 B at base +
+// 1: the rows kernel hashes each block's window, the W bytes that end at
 // the first 16-B boundary at or after the block's end (crc_rows_kernel OPT
-// bit 13: aligned 1 KiB rows at W's plan), each CRC corrected for the bytes
-// where window and block differ when the wave stores 64 of them
-// (crc_device.inc s_winimg).  The head split goes first (4-byte aligned B = h +
-// whole KiB rows).  PRISKV_CRC_WINDOW=0 turns it off (the stride kernel /
+// bit 13: aligned rows at W's plan), each CRC corrected for the bytes where
+// window and block differ when the wave stores 64 of them (crc_device.inc
+// s_winimg).  It goes before the head split, which keeps the
+// multiples of 4 it does not reach (heads of 49-64 B, W above 16 KiB).
+// PRISKV_CRC_WINDOW=0 turns it off (the head split, stride kernel or
 // extents path).
 constexpr uint32_t kWinMaxBytes = 16u << 10, kWinOver = 48;
 constexpr uint32_t kStrideMax = 9u << 10; // the stride / extents kernels' boundary (stride_to_extents)
@@ -1342,11 +1352,14 @@ int launch_blocks(const priskv_crc_ctx *ctx, const uint8_t *base, uint64_t nbloc
     const int path = choose_path(base, bs);
     if (path == PATH_ROWS)
         return launch_rows(ctx, base, nblocks, bs, out, s);
-    if (path == PATH_STRIDE && head_split(ctx, base, nblocks, bs))
-        return launch_head_split(ctx, base, nblocks, bs, out, s);
+    // the window mode before the head split: level or faster wherever both
+    // apply (profiles/r05/window/headsplit_vs_window.jsonl: 1064 B +13 %,
+    // 2056 / 3080 B +3-4 %, 4104 / 4144 B +2 %, 1040 B level)
     if (path == PATH_STRIDE)
         if (const uint32_t W = window_bytes(ctx, base, nblocks, bs))
             return launch_window(ctx, base, nblocks, bs, W, out, s);
+    if (path == PATH_STRIDE && head_split(ctx, base, nblocks, bs))
+        return launch_head_split(ctx, base, nblocks, bs, out, s);
     if (path == PATH_STRIDE && !stride_to_extents(base, bs))
         return launch_stride(ctx, base, nblocks, bs, out, s);
     if (path == PATH_STRIDE) // from 9 KiB: extents (segmented when few)
@@ -1463,10 +1476,10 @@ int priskv_crc32_blocks_path(const void *d_base, uint64_t nblocks, uint32_t bloc
     // a default context hashes B = h + whole KiB rows as bodies + heads
     // (unless few large blocks), and sends stride sizes from 9 KiB to the
     // extents kernel
-    if (path == PATH_STRIDE && head_split(nullptr, d_base, nblocks, block_size))
-        return PATH_HEAD;
     if (path == PATH_STRIDE && window_bytes(nullptr, d_base, nblocks, block_size))
         return PATH_WINDOW;
+    if (path == PATH_STRIDE && head_split(nullptr, d_base, nblocks, block_size))
+        return PATH_HEAD;
     if (path == PATH_STRIDE && stride_to_extents(d_base, block_size))
         return PATH_EXTENTS;
     return path;
@@ -1478,9 +1491,9 @@ int priskv_crc32_blocks_plan(const priskv_crc_ctx *ctx, const void *d_base, uint
     if (!ctx || block_size == 0 || !buf || len == 0)
         return -EINVAL;
     int path = choose_path(d_base, block_size);
-    if (path == PATH_STRIDE && head_split(ctx, d_base, nblocks, block_size))
-        path = PATH_HEAD;
     const uint32_t win = path == PATH_STRIDE ? window_bytes(ctx, d_base, nblocks, block_size) : 0u;
+    if (!win && path == PATH_STRIDE && head_split(ctx, d_base, nblocks, block_size))
+        path = PATH_HEAD;
     int w = 0;
     const char *fused_name = "crc_ranges_fused_kernel (few large values: segments, one launch)";
     if (win) {

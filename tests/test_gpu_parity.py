@@ -607,7 +607,8 @@ def test_ranges_many_per_wave_shapes(torch_cuda, any_ctx):
     assert np.array_equal(got, want), np.nonzero(got != want)[0][:8]
 
 
-@pytest.mark.parametrize("bs", [1028, 1024 + 64, 4100, 4104, 4096 + 64, 8196, (64 << 10) + 4, (1 << 20) + 4])
+@pytest.mark.parametrize("bs", [1028, 1024 + 64, 4100, 4104, 4096 + 52, 4096 + 64, 8196, 8192 + 52, 9220,
+                                (12 << 10) + 52, (16 << 10) + 52, (64 << 10) + 4, (1 << 20) + 4])
 def test_head_split_blocks(torch_cuda, ctx, bs):
     """Block sizes of whole KiB rows plus a 4-64 B head on 4-byte aligned
     bases: the rows kernel hashes the bodies in place (stride = block size)
@@ -630,8 +631,12 @@ def test_head_split_blocks(torch_cuda, ctx, bs):
                 torch.cuda.synchronize()
                 got = _u32(out)
                 assert np.array_equal(got, want), (bs, nb, shift, plan, np.nonzero(got != want)[0][:8])
-        if nb >= 2049 and bs < (16 << 10):  # bodies too short to segment: always the head split
-            assert "crc_head_kernel" in ctx.blocks_plan(t.data_ptr(), nb, bs), plan
+        if nb >= 2049 and bs < (16 << 10):  # bodies too short to segment: the head split, unless windows
+            from priskv_amd import blocks_path
+            want_path = blocks_path(t.data_ptr(), nb, bs)
+            plan = ctx.blocks_plan(t.data_ptr(), nb, bs)
+            assert ("crc_head_kernel" in plan) == (want_path == "headsplit"), plan
+            assert ("windows" in plan) == (want_path == "window"), plan
         del t
     off_ctx.close()
 
@@ -659,7 +664,8 @@ def test_head_split_few_large_odd_kib_bodies(torch_cuda, ctx, bs):
         assert np.array_equal(got, want), (bs, nb, np.nonzero(got != want)[0][:8])
         del t
     nbal = 2 * torch.cuda.get_device_properties(0).multi_processor_count * 8  # two blocks per rows-kernel wave
-    assert "crc_head_kernel" in ctx.blocks_plan(4096, nbal, bs)
+    body = bs - bs % 1024  # (round 5: the head split only on bodies of whole 4 KiB chunks)
+    assert ("crc_head_kernel" in ctx.blocks_plan(4096, nbal, bs)) == (body % 4096 == 0)
 
 
 def test_ranges_many_shape_chunk_sizes(torch_cuda, ctx):
@@ -1326,10 +1332,11 @@ def test_blocks_plan_strings(torch_cuda, ctx):
     assert ctx.blocks_plan(base + 1, 100, 4200).startswith("crc_stride_kernel<G=32,CH=8,NBUF=2,nt,progress-priority 3> "
                                                            "(9 rows of 512 B "
                                                            "per block, 408 B in front)")
-    # whole KiB rows + a 4-64 B head on a 4-byte aligned base: rows kernel + head terms
-    assert ctx.blocks_plan(base, 100, 4100) == ("crc_rows_kernel<G=64,CH=4,NBUF=3,nt,pipelined-fold,nibble-fold,"
-                                                "progress-priority 3> on the 4096-B bodies + crc_head_kernel "
-                                                "(4-B heads)")
+    # whole KiB rows + a 49-64 B head on a 4-byte aligned base (4-48 B: the
+    # window mode, above): rows kernel + head terms
+    assert ctx.blocks_plan(base, 100, 12340) == ("crc_rows_kernel<G=64,CH=4,NBUF=2,nt,progress-priority 1> on the "
+                                                 "12288-B bodies + crc_head_kernel (52-B heads)")
+    assert "(4096-B windows" in ctx.blocks_plan(base, 100, 4100)
     assert ctx.blocks_plan(base, 100, 520).startswith("crc_stride_kernel<G=16,CH=8,NBUF=2,nt,progress-priority 3> (3 rows of 256 B")
     assert ctx.blocks_plan(base, 100, 100).startswith("crc_stride_kernel<G=8,CH=8,NBUF=2,nt,byte-fold,progress-priority 3> (1 rows of 128 B")
     # the extents kernel from 9 KiB, odd sizes and multiples of 4 alike
@@ -1344,7 +1351,8 @@ def test_blocks_plan_strings(torch_cuda, ctx):
     assert ctx.blocks_plan(base, 100, 9212).startswith("crc_stride_kernel<G=32,CH=8,NBUF=2,nt,progress-priority 3> (18 rows of 512 B")
     assert ctx.blocks_plan(base, 100, 8700).startswith("crc_stride_kernel<G=32,CH=8,NBUF=2,nt,progress-priority 3> (17 rows of 512 B")
     assert ctx.blocks_plan(base, 100, 9300) == "crc_ranges_kernel (extents)"
-    assert "crc_head_kernel (4-B heads)" in ctx.blocks_plan(base, 100, 9220)
+    assert "crc_head_kernel (52-B heads)" in ctx.blocks_plan(base, 100, 16436)
+    assert ctx.blocks_plan(base, 100, 9220) == "crc_ranges_kernel (extents)"
     assert ctx.blocks_plan(base, 100, 15) == "crc_generic_kernel"
 
 

@@ -232,7 +232,7 @@ def test_path_selection():
     assert C.blocks_path(4104, 10, 4096) == "window"    # 8-byte aligned only
     assert C.blocks_path(4096, 10, 4081) == "window"
     assert C.blocks_path(4096, 10, 4080) == "stride"
-    assert C.blocks_path(4096, 10, 4144) == "headsplit"   # the head split goes first
+    assert C.blocks_path(4096, 10, 4144) == "window"      # before the head split
     assert C.blocks_path(4097, 10, 4144) == "window"
     assert C.blocks_path(4096, 10, 4145) == "stride"
     assert C.blocks_path(4096, 10, 8191) == "window"
@@ -242,7 +242,7 @@ def test_path_selection():
     # other whole-KiB multiples W >= 1 KiB (four blocks per wave group)
     assert C.blocks_path(4096, 10, 1023) == "window"
     assert C.blocks_path(4096, 10, 1071) == "window"
-    assert C.blocks_path(4096, 10, 1072) == "headsplit"    # the head split goes first
+    assert C.blocks_path(4096, 10, 1072) == "window"       # before the head split
     assert C.blocks_path(4096, 10, 1073) == "stride"
     assert C.blocks_path(4096, 10, 1008) == "stride"
     assert C.blocks_path(4096, 10, 2049) == "window"
@@ -250,10 +250,15 @@ def test_path_selection():
     assert C.blocks_path(4096, 10, 9215) == "stride"
     # whole KiB rows + a 4..64-B head (multiple of 4, 4-byte aligned base):
     # the rows kernel on the bodies + crc_head_kernel
-    assert C.blocks_path(4096, 10, 4100) == "headsplit"
-    assert C.blocks_path(4100, 10, 4100) == "headsplit"   # 4-byte aligned base
+    # (from round 5 the window mode takes those within 48 B of a whole KiB up to 16 KiB)
+    assert C.blocks_path(4096, 10, 4100) == "window"
+    assert C.blocks_path(4100, 10, 4100) == "window"      # 4-byte aligned base
+    assert C.blocks_path(4096, 10, 12288 + 52) == "headsplit"  # heads of 49-64 B on >= 12 KiB of 4 KiB chunks
+    assert C.blocks_path(4096, 10, 8192 + 52) == "stride"
+    assert C.blocks_path(4096, 10, 4096 + 52) == "stride"      # ... not on 4 KiB bodies (round 5)
+    assert C.blocks_path(4096, 10, 17408 + 4) == "extents"     # ... nor 17 KiB ones
     assert C.blocks_path(4098, 10, 4100) == "window"      # 2-byte aligned base
-    assert C.blocks_path(4096, 10, 1024 + 64) == "headsplit"
+    assert C.blocks_path(4096, 10, 1024 + 64) == "stride"     # (the head split until round 5)
     assert C.blocks_path(4096, 10, 1024 + 68) == "stride"  # head above 64 B
     # few large head + body blocks: the rows kernel does not segment the
     # bodies, so they keep the extents path (segmented by the fused kernel)
