@@ -200,8 +200,9 @@ int priskv_crc_fill_splitmix_dev(const priskv_crc_ctx *ctx, void *d_dst, uint64_
  * below 16 B: one thread per block), 7 = window (a block not a multiple
  * of 1 KiB on a 16-B aligned base, within W - 15 .. W + 48 B of a multiple
  * W of 4 KiB up to 16 KiB -- 4095, 4097, 4100, 8193 B, 4096 B on an odd
- * base -- or up to 48 B above another whole-KiB W below 9 KiB -- 1025,
- * 2049 B: the rows kernel on each block's 16-B aligned W-byte window, then
+ * base -- or, for sizes or bases that are not multiples of 4, up to 48 B
+ * above another whole-KiB W up to 6 KiB -- 1025, 2049 B: the rows kernel
+ * on each block's 16-B aligned W-byte window, then
  * the few bytes where window and block differ), 6 = head split (a multiple
  * of 4 that is whole 4 KiB chunks of at least 12 KiB plus a 4-64 B head on
  * a 4-byte aligned base, that the window does not take: the rows kernel on

@@ -1094,20 +1094,26 @@ constexpr int kWinOpt = 8192;
 uint32_t window_bytes(const priskv_crc_ctx *ctx, const void *base, uint64_t nblocks, uint32_t bs)
 {
     const uint32_t W = (uint32_t)(((uint64_t)bs + 15) / 1024 * 1024); // W - 15 <= bs
-    (void)base;
     (void)nblocks; // (blocks this small are never segmented: kSegMinLen)
     static_assert(kWinMaxBytes + kWinOver < kSegMinLen, "window sizes are never segmented");
     if ((ctx && !ctx->window) || W == 0 || W > kWinMaxBytes || bs > W + kWinOver)
         return 0;
-    // W not a multiple of 4 KiB (the G = 16 plans): only below 9 KiB, and
-    // there only where the stride kernel pads a whole extra row (B > W), or
-    // for W = 1 KiB below it.  Per ~4 GB call (profiles/r05/window/g16_*):
-    // 1025 B 843 -> 693 us, 2049 B 791 -> 687, 3073 B 673 -> 656, 1023 B
-    // 713 -> 682; but 2047 / 3071 / 6143 B level or slower, 2048 B on base
-    // + 1 643 -> 676, and from 9 KiB the extents kernel is faster (9217 B
-    // 644 against 649, 15361 B 602 against 633, 10239 B 639 against 667)
-    if (W % 4096 != 0 && (W >= kStrideMax || (W > 1024 && bs <= W) || (W == 1024 && bs == W)))
-        return 0;
+    // W not a multiple of 4 KiB (the G = 16 plans): only up to 6 KiB, only
+    // for sizes or bases that are not multiples of 4 (where the stride
+    // kernel funnel-shifts), and there only above W (where the stride kernel
+    // pads a whole extra row) or, for W = 1 KiB, below it.  Per ~4 GB call
+    // (profiles/r05/window/g16_*.jsonl, odd_sweep*.jsonl): 1025 B 843 -> 693
+    // us, 2049 B 791 -> 687, 3073 B 673 -> 656, 1023 B 713 -> 682, 1041 /
+    // 2065 / 3089 B +10 / +10 / +2 %; but multiples of 4 (1040, 2056, 3076,
+    // 5124 B: the stride kernel's aligned loads) 1-7 % slower, 2047 / 3071 /
+    // 6143 B level, 2048 B on base + 1 643 -> 676, 7169 B -1 %, and from 9
+    // KiB the extents kernel is faster (9217 B 644 against 649, 15361 B 602
+    // against 633)
+    if (W % 4096 != 0) {
+        const bool odd = (((uintptr_t)base | bs) & 3u) != 0;
+        if (!odd || W > 6144 || (W > 1024 && bs <= W) || (W == 1024 && bs == W))
+            return 0;
+    }
     return W;
 }
 

@@ -1679,9 +1679,10 @@ def test_stride_kernel_cost_model_sizes(torch_cuda, ctx, misalign):
 # block sizes within W - 15 .. W + 48 B of W = 4, 8, 12, 16 KiB: window mode
 _WINDOW_SIZES = [4081, 4095, 4096, 4097, 4099, 4111, 4112, 4127, 4144, 8177, 8191, 8193, 8240, 12287, 12300,
                  16369, 16383, 16385, 16432,
-                 # other whole-KiB W below 9 KiB (G = 16: four blocks per wave group),
-                 # B > W or W = 1 KiB
-                 1009, 1023, 1025, 1071, 1072, 2049, 3073, 6145, 7169, 8239]
+                 8239,
+                 # other whole-KiB W up to 6 KiB (G = 16: four blocks per wave group), sizes
+                 # or bases not multiples of 4, B > W or W = 1 KiB
+                 1009, 1023, 1025, 1071, 1072, 2049, 3073, 5121, 6145]
 
 
 @pytest.mark.parametrize("bs", _WINDOW_SIZES)
@@ -1705,9 +1706,11 @@ def test_window_blocks(torch_cuda, ctx, bs):
         for shift in (1, 3, 8, 13, 15) if bs % 1024 == 0 else (0, 1, 7, 12, 15):
             view = t[shift:shift + bs * nb]
             plan = ctx.blocks_plan(view.data_ptr(), nb, bs)
-            head = bs % 4 == 0 and (view.data_ptr() & 3) == 0 and 4 <= bs % 1024 <= 64
-            if not head:
+            from priskv_amd import blocks_path
+            if blocks_path(view.data_ptr(), nb, bs) == "window":  # (else a multiple of 4 the stride kernel takes)
                 assert plan.startswith(f"crc_rows_kernel<G={G},") and f"{W}-B windows" in plan, (bs, shift, plan)
+            else:
+                assert G == 16 and bs % 4 == 0 and (view.data_ptr() & 3) == 0, (bs, shift, plan)
             want = O.crc32_blocks(view.cpu().numpy(), bs, nthreads=8)
             for c in (ctx, off_ctx) if nb <= 2049 else (ctx,):
                 out = torch.full((nb,), sentinel, dtype=torch.int32, device="cuda")

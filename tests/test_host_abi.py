@@ -242,7 +242,8 @@ def test_path_selection():
     # other whole-KiB multiples W >= 1 KiB (four blocks per wave group)
     assert C.blocks_path(4096, 10, 1023) == "window"
     assert C.blocks_path(4096, 10, 1071) == "window"
-    assert C.blocks_path(4096, 10, 1072) == "window"       # before the head split
+    assert C.blocks_path(4096, 10, 1072) == "stride"       # a multiple of 4 on a G16 W: the stride kernel
+    assert C.blocks_path(4097, 10, 1072) == "window"       # ... on an odd base: the window
     assert C.blocks_path(4096, 10, 1073) == "stride"
     assert C.blocks_path(4096, 10, 1008) == "stride"
     assert C.blocks_path(4096, 10, 2049) == "window"
@@ -279,7 +280,8 @@ def test_path_selection():
     assert C.blocks_path(4097, 10, 9216) == "extents"   # 9 KiB on an odd base
     assert C.blocks_path(4097, 10, 2048) == "stride"    # B = W (not 4 KiB) on an odd base
     assert C.blocks_path(4097, 10, 8192) == "window"    # ... a 4 KiB multiple does window
-    assert C.blocks_path(4096, 10, 7169) == "window"
+    assert C.blocks_path(4096, 10, 7169) == "stride"       # G16 windows stop at 6 KiB
+    assert C.blocks_path(4096, 10, 6145) == "window"
     assert C.blocks_path(4096, 10, 9300) == "extents"   # odd from 9 KiB
     assert C.blocks_path(4097, 10, 9300) == "extents"   # unaligned base counts as odd
     assert C.blocks_path(4096, 10, 9212) == "stride"

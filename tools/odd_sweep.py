@@ -38,7 +38,9 @@ def ctx_env(**kv):
 SIZES = [1000, 1009, 1023, 1025, 1072, 1500, 2000, 2047, 2049, 2100, 3000, 3071, 3073, 4000, 4081, 4095, 4097,
          4111, 4200, 5000, 5121, 6000, 6143, 6145, 7169, 8000, 8191, 8193, 9000, 9217, 10000, 12287, 12289, 16383,
          16385]
-CASES = [(bs, 0) for bs in SIZES] + [(1024, 1), (2048, 1), (4096, 1), (4096, 8), (8192, 1), (4100, 1), (4100, 0)]
+# (three aligned 4 KiB cases first: the first seconds of a process run slow, clocks ramping)
+CASES = [(4096, 0)] * 3 + [(bs, 0) for bs in SIZES] + [(1024, 1), (2048, 1), (4096, 1), (4096, 8), (8192, 1),
+                                                      (4100, 1), (4100, 0), (1088, 0), (12340, 0), (65540, 0)]
 if os.environ.get("ODD_SWEEP_CASES"):  # "bs:off,bs:off,..."
     CASES = [tuple(int(x) for x in c.split(":")) for c in os.environ["ODD_SWEEP_CASES"].split(",")]
 out = open(sys.argv[1], "w") if len(sys.argv) > 1 else sys.stdout
