@@ -21,6 +21,9 @@ timed region, with barrier + max over ranks at N > 1):
   tib           configs[3]: each rank's 2 Mi x 64 KiB = 128 GiB shard of the
                 16 Mi x 64 KiB (1 TiB at 8 GPUs) region; sampled parity
                 (first, last, every 4096th block of every shard)
+  odd           1 M x 4095 B and 1 M x 4097 B blocks per rank (odd sizes the
+                server's -v accepts; the rows kernel's window mode), sampled
+                parity, traffic from profiles/ when measured
   streamed      configs[4]: the headline's 1 Mi x 4 KiB blocks from HOST
                 memory, end to end (H2D copies, kernels and D2H of the CRCs
                 overlapped on 3 streams, priskv_crc32_blocks_host): pinned
@@ -78,8 +81,12 @@ CONFIGS = {
     "sweep64k": (65536, 1 << 16, "64Ki x 64KiB value blocks per GPU, device-resident (4 GiB/GPU; BASELINE configs[2])"),
     "sweep1m": (1 << 20, 1 << 12, "4Ki x 1MiB value blocks per GPU, device-resident (4 GiB/GPU; BASELINE configs[2])"),
     "tib": (65536, 1 << 21, "2Mi x 64KiB value blocks per GPU (128 GiB/GPU; 1 TiB at 8 GPUs; BASELINE configs[3])"),
+    # odd block sizes the server's -v also accepts (server/server.c:236-244): the window mode
+    "odd4095": (4095, 1000000, "1M x 4095 B value blocks per GPU, device-resident (odd size: the window mode)"),
+    "odd4097": (4097, 1000000, "1M x 4097 B value blocks per GPU, device-resident (odd size: the window mode)"),
 }
 SWEEP = (("64KiB", "sweep64k"), ("1MiB", "sweep1m"))
+ODD = (("4095", "odd4095"), ("4097", "odd4097"))
 
 
 def parse(argv=None):
@@ -98,6 +105,7 @@ def parse(argv=None):
     p.add_argument("--no-sweep", action="store_true", help="skip the configs[2] (64 KiB / 1 MiB) legs")
     p.add_argument("--sweep-steps", type=int, default=20)
     p.add_argument("--no-streamed", action="store_true", help="skip the configs[4] (host-resident) leg")
+    p.add_argument("--no-odd", action="store_true", help="skip the odd block size legs (4095 / 4097 B)")
     p.add_argument("--streamed-steps", type=int, default=5)
     return p.parse_args(argv)
 
@@ -638,6 +646,9 @@ def main():
         result["sweep"] = {k: leg(f"sweep_{k}", resident_leg, B, name, args.sweep_steps) for k, name in SWEEP}
     if not args.no_tib and args.config == "default":
         result["tib"] = leg("tib", resident_leg, B, "tib", args.tib_steps, parity="sampled")
+    if not args.no_odd and args.config == "default":
+        result["odd"] = {k: leg(f"odd_{k}", resident_leg, B, name, args.sweep_steps, parity="sampled")
+                         for k, name in ODD}
     if not args.no_streamed:
         result["streamed"] = leg("streamed", streamed_leg, B, host, bs, want)
     # cold passes LAST on the GPU: what a one-off recovery scrub sees (clock
