@@ -7,8 +7,11 @@
  * server/kv.c:408 (priskv_insert_keynode), server/rdma.c:764
  * (priskv_tiering_req_new).
  *
- * Implemented on the host in priskv_amd/csrc/crc_host.c (slice-by-8, bit-exact
- * with server/crc.c:90-109: reflected 0xEDB88320, init 0, no final xor).  This
+ * Implemented on the host in priskv_amd/csrc/crc_host.c, bit-exact with
+ * server/crc.c:90-109 (reflected 0xEDB88320, init 0, no final xor): a
+ * VPCLMULQDQ or PCLMULQDQ fold for longer inputs where the CPU has it
+ * (crc_host_clmul.c, chosen once from cpuid), slice-by-8 tables otherwise
+ * and for short inputs.  This
  * symbol hashes keys (<= 1 KiB, server/rdma.h:49) synchronously on the RDMA
  * completion path, where a GPU launch would cost more than the work; the
  * batched value-block checksum runs on the GPU through priskv_crc_gpu.h.

@@ -59,12 +59,17 @@ void priskv_crc_ctx_destroy(priskv_crc_ctx *ctx);
 int priskv_crc_ctx_device(const priskv_crc_ctx *ctx);
 
 /* Hand the scratch-pool slots `stream` owns back to the context's pool
- * (a slot belongs to the first stream that takes it; hipStreamPerThread's
- * belong to the calling thread).  Waits for the stream's work first.  Call
- * it before destroying a stream that ran *_dev calls -- or from a thread
- * about to exit that used hipStreamPerThread -- while no other thread
- * submits to that stream.  Optional: a stream that finds the pool full also
- * takes over slots of streams that have no work left.  0 / -EINVAL / -EIO. */
+ * (a slot belongs to the first stream that takes it, by hipStreamGetId;
+ * hipStreamPerThread is a different stream on every thread).  Waits for the
+ * stream's work first, and frees the scratch of destroyed graphs.  Call it
+ * before destroying a stream that ran *_dev calls -- or from a thread about
+ * to exit that used hipStreamPerThread -- while no other thread submits to
+ * that stream.  Without it the slots of a destroyed stream return to the
+ * pool only if the pool was contended when that stream last used them (the
+ * library then marked each use's end with its own event); otherwise they
+ * stay out of use until ctx_destroy and calls that find no slot allocate
+ * per call on their stream.  The library never passes another caller's
+ * stream to HIP.  0 / -EINVAL / -ENODEV / -EIO. */
 int priskv_crc_stream_release(const priskv_crc_ctx *ctx, void *stream);
 
 /* Device-resident batch: d_base -> nblocks * block_size bytes of device

@@ -30,6 +30,7 @@
 // built by ONE v_perm_b32 (byte1 <- x byte t, byte0 <- per-lane constant).
 #include <hip/hip_runtime.h>
 
+#include <dlfcn.h>
 #include <errno.h>
 #include <pthread.h>
 #include <stdint.h>
@@ -60,10 +61,12 @@ namespace {
 struct priskv_crc_pool_slot {
     void *p;
     size_t size;
-    hipStream_t home; // the one stream that uses the slot
-    pthread_t tid;    // home == hipStreamPerThread: the host thread whose stream it is
-    int homed;        // home is set (the slot has been taken once)
-    int busy;         // taken by a call in flight on the host
+    unsigned long long home; // the one stream that uses the slot (StreamKey)
+    pthread_t tid;           // ... and its host thread, for a per-thread stream keyed by handle
+    int homed;               // home is set (the slot has been taken once)
+    int busy;                // taken by a call in flight on the host
+    int armed;               // ev was recorded after the slot's last use (pool contended)
+    hipEvent_t ev;           // the library's own event (created on first need)
 };
 
 struct priskv_crc_ctx {
@@ -109,6 +112,9 @@ struct priskv_crc_ctx {
     // the fused few-extents kernel's counters + partials (zeroed when
     // allocated; the kernel leaves the counters zero; guarded by pool_lock)
     mutable priskv_crc_pool_slot cnt_pool[NPOOL];
+    mutable uint64_t pool_calls;     // pooled takes so far (guarded by pool_lock)
+    mutable uint64_t pool_last_miss; // pool_calls at the last take that found no slot (0: never)
+    mutable uint64_t pool_misses, pool_takeovers; // diagnostics (priskv_crc_cov_pool, test-only build)
     int fused;                 // few extents in one launch (PRISKV_CRC_FUSED=0: the three-launch path)
 };
 
@@ -164,31 +170,38 @@ inline int herr(hipError_t e)
 // Scratch for one *_dev call.  Outside stream capture it comes from the
 // context's pool, which saves the stream-ordered alloc/free pair (~6 us of
 // host time per call, profiles/r01/host_cost_r4k.json).  A slot belongs to
-// the first stream that takes it and only that stream takes it again, so
-// stream order alone puts its previous use first -- no event.  (A handle
-// stays taken while its stream has work: a destroyed stream's object lives
-// until that work completes, so a new stream cannot alias it meanwhile.)
-// hipStreamPerThread names a different stream on every host thread, so its
-// slots belong to (handle, thread).  A stream that finds no slot of its own
-// and none unowned takes over a free slot whose stream has no work left
-// (hipStreamQuery), so slots of streams a server has destroyed return to the
-// pool; priskv_crc_stream_release hands a stream's slots back explicitly
-// (the only way for a hipStreamPerThread thread that is about to exit).
-// Rounds 1-3 recorded an event per release so that any stream could take
-// any slot: that marker packet idled the queue ~5 us before the next
-// call's kernel (1 x 256 MiB 54.7 -> 49.9 us per call without it; also with
-// the event carried by the kernel launch itself, hipExtLaunchKernel, 4.6 us:
-// profiles/r04/pool_event/).  With no free slot of the stream's own or
-// unowned (more concurrent streams than slots), or with the pool off, it is
-// a per-call hipMallocAsync / hipFreeAsync.
+// the first stream that takes it (StreamKey: hipStreamPerThread is a
+// different owner on every thread) and only that stream takes it again, so
+// stream order alone puts its previous use first: no event while every
+// stream finds a slot.  The library passes no stream to HIP but the one its
+// caller handed it in the current call.
+//
+// Takeover (more streams than slots).  A take that finds no free slot of its
+// stream and none unowned marks the pool contended; from then on, until
+// kArmCalls pooled takes pass without another miss, each release records the
+// slot's own event on the releasing stream before it frees the slot ("armed")
+// -- the ~5 us marker rounds 1-3 paid on every call (1 x 256 MiB 54.7 ->
+// 49.9 us without it, profiles/r04/pool_event/), now paid only under
+// contention.  A stream with no slot takes over a free slot whose armed event
+// has completed (hipEventQuery on the library's own event: every use of the
+// slot is finished, whether its stream still exists, was destroyed with work
+// in flight, or is being captured on another thread).  An unarmed slot of
+// another stream is never taken: a stream destroyed without
+// priskv_crc_stream_release while the pool was uncontended keeps its slots
+// until the context is destroyed, and calls that find no slot take a per-call
+// hipMallocAsync / hipFreeAsync on their stream -- a smaller pool, never a
+// shared slot.  (Round 5 took over any slot whose home handle hipStreamQuery
+// did not report busy: a destroyed handle's error read as idle while its work
+// could still run, and querying a stream another thread was capturing broke
+// that capture.)  Pool calls run in relaxed capture mode, so another thread's
+// global-mode capture does not turn them into errors.
 //
 // While the stream is capturing, the scratch is a plain device allocation
-// the captured graph owns (graph_scratch): graph memory nodes (hipMallocAsync
-// inside a capture) returned wrong CRCs in round 5 -- the first three
-// back-to-back launches of a freshly captured graph, after other graphs of
-// the process had been destroyed, left 6-16 of 1900 split-mode blocks wrong
-// in most processes, and the same graph with dedicated memory did not
-// (tools/graph_race_probe.py).
+// the captured graph owns (graph_scratch).  Round 5 replaced graph memory
+// nodes (hipMallocAsync inside a capture) with it after 6-16 of 1900
+// split-mode blocks came back wrong in graphs with memory-node scratch
+// (tools/graph_race_probe.py; the two-word finish that failed
+// there is now one word, finish_shared in crc_device.inc).
 //
 // zero: the memory must read as zeros when a call gets it.  Then `slots` is a
 // pool whose users leave their slot zeroed (the fused extents kernel's
@@ -199,17 +212,23 @@ constexpr int kGraphOwned = -2; // Scratch::slot of a captured call's graph-owne
 // relaxed capture mode, so a global-mode capture is not invalidated) tied to
 // the graph being captured by a user object, whose destructor runs when the
 // graph and every instantiation of it are gone.  Destructors must not call
-// HIP, so it queues the buffer; priskv_crc calls outside capture (and
-// ctx_destroy) free the queue.  One buffer per captured call: launches of one
-// graph exec are ordered, so only two instantiations of one graph launched
-// concurrently could share it (documented in the header).
+// HIP, so it queues the buffer; calls outside capture free the queue once it
+// holds kDeferBatch buffers or kDeferBytes (hipFree synchronises the device:
+// not on every call after a graph is destroyed), and ctx_destroy /
+// priskv_crc_stream_release free whatever is queued.  One buffer per captured
+// call: launches of one graph exec are ordered, so only two instantiations of
+// one graph launched concurrently could share it (documented in the header).
 struct DeferredFree {
     void *p;
     int device;
+    size_t bytes;
 };
 pthread_mutex_t g_defer_lock = PTHREAD_MUTEX_INITIALIZER;
 std::vector<DeferredFree> g_deferred;
 volatile int g_deferred_n = 0;
+volatile size_t g_deferred_bytes = 0;
+constexpr int kDeferBatch = 16;
+constexpr size_t kDeferBytes = 256u << 20;
 
 void graph_scratch_release(void *arg)
 {
@@ -218,6 +237,7 @@ void graph_scratch_release(void *arg)
     try {
         g_deferred.push_back(*d);
         g_deferred_n = (int)g_deferred.size();
+        g_deferred_bytes = g_deferred_bytes + d->bytes;
     } catch (...) { // out of host memory: leak the buffer rather than call HIP here
     }
     pthread_mutex_unlock(&g_defer_lock);
@@ -226,10 +246,10 @@ void graph_scratch_release(void *arg)
 
 // free the buffers of destroyed graphs (outside capture: hipFree
 // synchronises; relaxed mode, so another thread's global-mode capture does
-// not make it an error)
-void free_deferred()
+// not make it an error).  force = false: only once the queue is full.
+void free_deferred(bool force)
 {
-    if (!g_deferred_n)
+    if (!g_deferred_n || (!force && g_deferred_n < kDeferBatch && g_deferred_bytes < kDeferBytes))
         return;
     hipStreamCaptureMode mode = hipStreamCaptureModeRelaxed;
     (void)hipThreadExchangeStreamCaptureMode(&mode);
@@ -237,6 +257,7 @@ void free_deferred()
     pthread_mutex_lock(&g_defer_lock);
     todo.swap(g_deferred);
     g_deferred_n = 0;
+    g_deferred_bytes = 0;
     pthread_mutex_unlock(&g_defer_lock);
     int old = -1;
     (void)hipGetDevice(&old);
@@ -267,7 +288,7 @@ int graph_scratch(const priskv_crc_ctx *ctx, hipStream_t s, size_t bytes, void *
     (void)hipThreadExchangeStreamCaptureMode(&mode);
     if (rc)
         return rc;
-    DeferredFree *d = new (std::nothrow) DeferredFree{p, ctx->device};
+    DeferredFree *d = new (std::nothrow) DeferredFree{p, ctx->device, bytes ? bytes : 4};
     hipUserObject_t obj = nullptr;
     if (!d || hipUserObjectCreate(&obj, d, graph_scratch_release, 1, hipUserObjectNoDestructorSync) != hipSuccess) {
         delete d;
@@ -284,6 +305,68 @@ int graph_scratch(const priskv_crc_ctx *ctx, hipStream_t s, size_t bytes, void *
     *out = p;
     return 0;
 }
+
+// Which stream a pool slot belongs to.  With a HIP runtime that has
+// hipStreamGetId (7.1 and later; looked up at run time, since the runtime a
+// process loads -- e.g. the one PyTorch ships -- may be older) the stream's
+// id, which names one stream for its whole life.  Otherwise the handle, and
+// for hipStreamPerThread -- one handle naming a different stream on every
+// host thread -- the handle and the thread.  A handle can name a new stream
+// after the old one is destroyed; HIP's hipStreamDestroy waits for the
+// stream's work before it frees the stream (checked on the box:
+// tests/test_gpu_pool_contention.py::test_stream_destroy_waits_for_its_work),
+// so the new owner's calls cannot overlap the old one's.
+struct StreamKey {
+    unsigned long long v = 0;
+    bool per_thread = false;
+    pthread_t tid{};
+};
+
+typedef hipError_t (*StreamGetIdFn)(hipStream_t, unsigned long long *);
+StreamGetIdFn stream_get_id_fn()
+{
+    static StreamGetIdFn fn = [] {
+        Dl_info di;
+        if (!dladdr(reinterpret_cast<void *>(&hipStreamQuery), &di) || !di.dli_fname)
+            return (StreamGetIdFn) nullptr;
+        void *h = dlopen(di.dli_fname, RTLD_LAZY | RTLD_NOLOAD);
+        StreamGetIdFn f = h ? reinterpret_cast<StreamGetIdFn>(dlsym(h, "hipStreamGetId")) : nullptr;
+        if (h)
+            dlclose(h); // (RTLD_NOLOAD: drops only this reference)
+        return f;
+    }();
+    return fn;
+}
+
+bool stream_key(hipStream_t s, StreamKey *k)
+{
+    if (StreamGetIdFn f = stream_get_id_fn())
+        return f(s, &k->v) == hipSuccess;
+    k->v = (unsigned long long)(uintptr_t)s;
+    k->per_thread = s == hipStreamPerThread;
+    k->tid = pthread_self();
+    return true;
+}
+
+bool slot_owned_by(const priskv_crc_pool_slot &q, const StreamKey &k)
+{
+    return q.homed && q.home == k.v && (!k.per_thread || pthread_equal(q.tid, k.tid));
+}
+
+// the calling thread in relaxed capture mode for the guard's lifetime
+struct RelaxedCapture {
+    hipStreamCaptureMode mode = hipStreamCaptureModeRelaxed;
+    bool ok;
+    RelaxedCapture() : ok(hipThreadExchangeStreamCaptureMode(&mode) == hipSuccess) {}
+    ~RelaxedCapture()
+    {
+        if (ok)
+            (void)hipThreadExchangeStreamCaptureMode(&mode);
+    }
+};
+
+// pooled takes after the last miss during which releases stay armed
+constexpr uint64_t kArmCalls = 1024;
 
 struct Scratch {
     const priskv_crc_ctx *ctx;
@@ -303,6 +386,40 @@ struct Scratch {
         const uint32_t grid = (uint32_t)(nw / 256 + 1 < 1024 ? nw / 256 + 1 : 1024);
         return launch_k(crc_zero_kernel, dim3(grid), dim3(256), s, static_cast<uint32_t *>(q), nw);
     }
+    // a free slot for stream id sid (pool_lock held), or -1
+    int pick(const StreamKey &key, size_t bytes) const
+    {
+        // free slots of this stream first, then unowned ones: the smallest
+        // that fits, else the largest (grown)
+        int fit[2] = {-1, -1}, grow[2] = {-1, -1};
+        for (int i = 0; i < NPOOL; i++) {
+            const priskv_crc_pool_slot &q = slots[i];
+            if (q.busy || (q.homed && !slot_owned_by(q, key)))
+                continue;
+            const int o = q.homed ? 0 : 1;
+            if (q.size >= bytes) {
+                if (fit[o] < 0 || q.size < slots[fit[o]].size)
+                    fit[o] = i;
+            } else if (grow[o] < 0 || q.size > slots[grow[o]].size) {
+                grow[o] = i;
+            }
+        }
+        int k = fit[0] >= 0 ? fit[0] : fit[1] >= 0 ? fit[1] : grow[0] >= 0 ? grow[0] : grow[1];
+        if (k >= 0)
+            return k;
+        // none: the pool is contended; take over a free slot whose armed
+        // event has completed (its last use is finished)
+        ctx->pool_last_miss = ctx->pool_calls;
+        ctx->pool_misses++;
+        for (int i = 0; i < NPOOL; i++) {
+            const priskv_crc_pool_slot &q = slots[i];
+            if (!q.busy && q.armed && q.ev && hipEventQuery(q.ev) == hipSuccess) {
+                ctx->pool_takeovers++;
+                return i;
+            }
+        }
+        return -1;
+    }
     int get(size_t bytes)
     {
         hipStreamCaptureStatus cs = hipStreamCaptureStatusActive;
@@ -313,49 +430,20 @@ struct Scratch {
             slot = kGraphOwned;
             return zero ? zero_fill(p, bytes) : 0; // a kernel node: every replay starts from zeros
         }
+        RelaxedCapture relaxed;
         if (capt_ok && cs == hipStreamCaptureStatusNone)
-            free_deferred();
-        if (ctx->pool_ready && capt_ok && cs == hipStreamCaptureStatusNone) {
-            // hipStreamPerThread is one handle that names a different stream
-            // on every host thread: its slots belong to (handle, thread)
-            const bool pt = s == hipStreamPerThread;
-            const pthread_t self = pthread_self();
-            auto own = [&](const priskv_crc_pool_slot &q) {
-                return q.home == s && (!pt || pthread_equal(q.tid, self));
-            };
+            free_deferred(false);
+        StreamKey key;
+        if (ctx->pool_ready && capt_ok && cs == hipStreamCaptureStatusNone && stream_key(s, &key)) {
             pthread_mutex_lock(&ctx->pool_lock);
-            // free slots of this stream first, then unowned ones: the smallest
-            // that fits, else the largest (grown)
-            int fit[2] = {-1, -1}, grow[2] = {-1, -1};
-            for (int i = 0; i < NPOOL; i++) {
-                const priskv_crc_pool_slot &q = slots[i];
-                if (q.busy || (q.homed && !own(q)))
-                    continue;
-                const int o = q.homed ? 0 : 1;
-                if (q.size >= bytes) {
-                    if (fit[o] < 0 || q.size < slots[fit[o]].size)
-                        fit[o] = i;
-                } else if (grow[o] < 0 || q.size > slots[grow[o]].size) {
-                    grow[o] = i;
-                }
-            }
-            int k = fit[0] >= 0 ? fit[0] : fit[1] >= 0 ? fit[1] : grow[0] >= 0 ? grow[0] : grow[1];
-            // none: take over a free slot of another stream that has no work
-            // left (every use of the slot is complete; a destroyed stream's
-            // handle no longer names a live stream).  hipStreamPerThread homes
-            // cannot be queried from here and stay with their thread.
-            for (int i = 0; k < 0 && i < NPOOL; i++) {
-                const priskv_crc_pool_slot &q = slots[i];
-                if (q.busy || !q.homed || q.home == hipStreamPerThread)
-                    continue;
-                if (hipStreamQuery(q.home) != hipErrorNotReady)
-                    k = i;
-            }
+            ctx->pool_calls++;
+            const int k = pick(key, bytes);
             if (k >= 0) {
                 slots[k].busy = 1;
                 slots[k].homed = 1;
-                slots[k].home = s;
-                slots[k].tid = self;
+                slots[k].home = key.v;
+                slots[k].tid = key.tid;
+                slots[k].armed = 0; // an event of an earlier release says nothing about this use
             }
             pthread_mutex_unlock(&ctx->pool_lock);
             if (k >= 0) {
@@ -365,8 +453,8 @@ struct Scratch {
                     size_t cap = 64u << 10;
                     while (cap < bytes)
                         cap *= 2;
-                    if (q.p)
-                        rc = herr(hipFreeAsync(q.p, s)); // after the slot's last use: same stream, or none pending
+                    if (q.p) // after the slot's last use: same stream, or a completed armed event
+                        rc = herr(hipFreeAsync(q.p, s));
                     q.p = nullptr;
                     q.size = 0;
                     if (!rc && !(rc = herr(hipMallocAsync(&q.p, cap, s))))
@@ -395,10 +483,23 @@ struct Scratch {
     {
         if (slot == kGraphOwned) // the captured graph frees it
             return 0;
-        if (slot < 0)
+        if (slot < 0) {
+            RelaxedCapture relaxed;
             return p ? herr(hipFreeAsync(p, s)) : 0;
+        }
         priskv_crc_pool_slot &q = slots[slot];
         pthread_mutex_lock(&ctx->pool_lock);
+        const bool arm = ctx->pool_last_miss && ctx->pool_calls - ctx->pool_last_miss < kArmCalls;
+        pthread_mutex_unlock(&ctx->pool_lock);
+        bool armed = false;
+        if (arm) { // contended: mark this use's end (the slot is still busy, so nobody takes it meanwhile)
+            RelaxedCapture relaxed;
+            if (!q.ev && hipEventCreateWithFlags(&q.ev, hipEventDisableTiming) != hipSuccess)
+                q.ev = nullptr;
+            armed = q.ev && hipEventRecord(q.ev, s) == hipSuccess;
+        }
+        pthread_mutex_lock(&ctx->pool_lock);
+        q.armed = armed;
         q.busy = 0;
         pthread_mutex_unlock(&ctx->pool_lock);
         slot = -1;
@@ -687,11 +788,10 @@ uint32_t split_units_xw(const priskv_crc_ctx *ctx, int p, uint64_t n)
 }
 
 // stride: bytes from block to block (0: bs; more for the head-split bodies).
-// split > 1: the split mode (ngroups = blocks; cnt / xacc: zeroed scratch of
-// ngroups words each, left zero), one launch
+// split > 1: the split mode (ngroups = blocks; acc: zeroed scratch of
+// ngroups 64-bit words, left zero), one launch
 int launch_plan(const priskv_crc_ctx *ctx, int p, const uint8_t *base, uint64_t ngroups, uint32_t bs, uint32_t *out,
-                hipStream_t s, uint32_t stride = 0, uint32_t split = 1, uint32_t *cnt = nullptr,
-                uint32_t *xacc = nullptr)
+                hipStream_t s, uint32_t stride = 0, uint32_t split = 1, uint64_t *acc = nullptr)
 {
     if (!stride)
         stride = bs;
@@ -711,7 +811,7 @@ int launch_plan(const priskv_crc_ctx *ctx, int p, const uint8_t *base, uint64_t 
         uint32_t xw = split_units_xw(ctx, p, n), tile = 0;
         void *args[] = {(void *)&base, (void *)&n,    (void *)&bs,    (void *)&img,   (void *)&fold,
                         (void *)&out,  (void *)&xw,   (void *)&tile,  (void *)&stride, (void *)&split,
-                        (void *)&zp,   (void *)&cnt,  (void *)&xacc};
+                        (void *)&zp,   (void *)&acc};
         return herr(hipLaunchKernel(plan_fn(p, true), dim3(grid), dim3(64 * NW), args, 0, s));
     }
     // the kernel counts a wave's chunks in 32 bits: cap groups per launch
@@ -726,10 +826,10 @@ int launch_plan(const priskv_crc_ctx *ctx, int p, const uint8_t *base, uint64_t 
         uint32_t xw = n >= 32ull * grid * NW ? ctx->plan_xw[p] : 0u;
         uint32_t tile = tile_groups(ctx, n, nb_per_group * stride);
         uint32_t one = 1;
-        uint32_t *none = nullptr;
+        uint64_t *none = nullptr;
         void *args[] = {(void *)&b,  (void *)&n,    (void *)&bs,   (void *)&img,    (void *)&fold,
                         (void *)&o,  (void *)&xw,   (void *)&tile, (void *)&stride, (void *)&one,
-                        (void *)&zp, (void *)&none, (void *)&none};
+                        (void *)&zp, (void *)&none};
         if (int rc = herr(hipLaunchKernel(plan_fn(p), dim3(grid), dim3(64 * NW), args, 0, s)))
             return rc;
         done += n;
@@ -824,8 +924,7 @@ int launch_split(const priskv_crc_ctx *ctx, int p, const uint8_t *base, uint64_t
     Scratch sc(ctx, s, ctx->cnt_pool, true); // zero at rest: the kernel leaves it zero
     if (int rc = sc.get((size_t)nblocks * 8))
         return rc;
-    uint32_t *cnt = static_cast<uint32_t *>(sc.p);
-    const int rc = launch_plan(ctx, p, base, nblocks, bs, out, s, 0, S, cnt, cnt + nblocks);
+    const int rc = launch_plan(ctx, p, base, nblocks, bs, out, s, 0, S, static_cast<uint64_t *>(sc.p));
     const int frc = sc.release();
     return rc ? rc : frc;
 }
@@ -884,8 +983,8 @@ bool extents_segmented(const priskv_crc_ctx *ctx, uint64_t n, uint64_t max_len)
 }
 
 // the fused few-extents kernel, one launch (n <= kFusedMaxExtents): the plan
-// inside every workgroup; extents shared by workgroups finish through two
-// zero-at-rest words each (counter, XOR) that the kernel leaves zero
+// inside every workgroup; extents shared by workgroups finish through one
+// zero-at-rest 64-bit word each (count, XOR) that the kernel leaves zero
 int launch_fused(const priskv_crc_ctx *ctx, const uint8_t *base, uint64_t n, const uint64_t *offs,
                  const uint32_t *lens, uint64_t stride, uint32_t len_const, uint32_t *out, hipStream_t s)
 {
@@ -896,8 +995,7 @@ int launch_fused(const priskv_crc_ctx *ctx, const uint8_t *base, uint64_t n, con
     Scratch sc(ctx, s, ctx->cnt_pool, true);
     if (int rc = sc.get((size_t)kFusedMaxExtents * 8))
         return rc;
-    uint32_t *cnt = static_cast<uint32_t *>(sc.p);
-    uint32_t *xacc = cnt + kFusedMaxExtents;
+    uint64_t *acc = static_cast<uint64_t *>(sc.p);
     const uint64_t sh = (uintptr_t)base & 15;
     const uint8_t *abase = base - sh;
     const uint32_t *lens_or_null = offs ? lens : nullptr;
@@ -924,8 +1022,7 @@ int launch_fused(const priskv_crc_ctx *ctx, const uint8_t *base, uint64_t n, con
     const uint32_t *img = ctx->d_lds_image[0], *nib = ctx->d_nib16, *rs = ctx->d_rowshift, *zp = ctx->d_zpow;
     void *args[] = {(void *)&abase, (void *)&n,   (void *)&offs, (void *)&lens_or_null, (void *)&sh,
                     (void *)&stride, (void *)&len_const, (void *)&img, (void *)&nib, (void *)&rs,
-                    (void *)&out,   (void *)&zp,  (void *)&tgt, (void *)&ms, (void *)&cnt, (void *)&xacc,
-                    (void *)&xw};
+                    (void *)&out,   (void *)&zp,  (void *)&tgt, (void *)&ms, (void *)&acc, (void *)&xw};
     const int rc = herr(hipLaunchKernel(fn, dim3(grid), dim3(64 * nw), args, 0, s));
     const int frc = sc.release();
     return rc ? rc : frc;
@@ -1174,10 +1271,10 @@ int launch_window(const priskv_crc_ctx *ctx, const uint8_t *base, uint64_t nbloc
         const uint8_t *b = base + done * per * bs;
         uint32_t *o = out + done * per;
         uint32_t xw = n >= 32ull * grid * NW ? ctx->plan_xw[p] : 0u, tile = 0, one = 1, stride = bs, wb = W;
-        uint32_t *none = nullptr;
+        uint64_t *none = nullptr;
         void *args[] = {(void *)&b,  (void *)&n,    (void *)&wb,   (void *)&img,    (void *)&fold,
                         (void *)&o,  (void *)&xw,   (void *)&tile, (void *)&stride, (void *)&one,
-                        (void *)&zp, (void *)&none, (void *)&none};
+                        (void *)&zp, (void *)&none};
         if (int rc = herr(hipLaunchKernel(window_fn(p), dim3(grid), dim3(64 * NW), args, 0, s)))
             return rc;
         done += n;
@@ -1408,9 +1505,13 @@ int launch_blocks(const priskv_crc_ctx *ctx, const uint8_t *base, uint64_t nbloc
 // overrides every plan ("1:1" = equal split) and applies regardless.
 uint32_t xcd_weights(int xcd_rr, int p)
 {
-    uint32_t we = kPlans[p].we, wo = kPlans[p].wo;
+    // no round-robin dispatch found (another partition mode, the probe off):
+    // equal shares whatever the environment says -- the kernels' per-workgroup
+    // weight order (wave_range) is consistent across a launch only under
+    // round-robin dispatch
     if (!xcd_rr)
-        we = wo = 1;
+        return 0u;
+    uint32_t we = kPlans[p].we, wo = kPlans[p].wo;
     if (const char *e = getenv("PRISKV_CRC_XCD_WEIGHTS")) {
         unsigned a = 0, b = 0;
         if (sscanf(e, "%u:%u", &a, &b) == 2 && a && b && a < 65536 && b < 65536) {
@@ -1793,7 +1894,7 @@ void priskv_crc_ctx_destroy(priskv_crc_ctx *c)
     if (!c)
         return;
     DevGuard g(c->device);
-    free_deferred();
+    free_deferred(true);
     if (c->stream_ready) {
         for (int i = 0; i < NSTREAM; i++) {
             (void)hipStreamSynchronize(c->streams[i]);
@@ -1827,9 +1928,12 @@ void priskv_crc_ctx_destroy(priskv_crc_ctx *c)
         if (any)
             (void)hipDeviceSynchronize();
         for (priskv_crc_pool_slot *slots : {c->pool, c->cnt_pool})
-            for (int i = 0; i < NPOOL; i++)
+            for (int i = 0; i < NPOOL; i++) {
                 if (slots[i].p)
                     (void)hipFreeAsync(slots[i].p, c->aux);
+                if (slots[i].ev)
+                    (void)hipEventDestroy(slots[i].ev);
+            }
     }
     if (c->aux) {
         (void)hipStreamSynchronize(c->aux);
@@ -1842,6 +1946,45 @@ void priskv_crc_ctx_destroy(priskv_crc_ctx *c)
 
 int priskv_crc_ctx_device(const priskv_crc_ctx *ctx) { return ctx ? ctx->device : -EINVAL; }
 
+#ifdef PRISKV_CRC_COVERAGE
+// test-only build (make cov, tests/test_gpu_graphs_pool.py): after the device
+// is idle, out[0] = the groups the waves' ranges (wave_range) covered since the
+// last take, out[1] = the sum of their indices; then zero both.  Not declared
+// in include/ and absent from the product library.
+extern "C" __attribute__((visibility("default"))) int priskv_crc_cov_take(const priskv_crc_ctx *ctx, uint64_t *out)
+{
+    if (!ctx || !out)
+        return -EINVAL;
+    DevGuard g(ctx->device);
+    unsigned long long h[2] = {0, 0};
+    if (int rc = herr(hipDeviceSynchronize()))
+        return rc;
+    if (int rc = herr(hipMemcpyFromSymbol(h, HIP_SYMBOL(g_cov), sizeof(h))))
+        return rc;
+    const unsigned long long z[2] = {0, 0};
+    if (int rc = herr(hipMemcpyToSymbol(HIP_SYMBOL(g_cov), z, sizeof(z))))
+        return rc;
+    out[0] = h[0];
+    out[1] = h[1];
+    return 0;
+}
+
+// test-only build: the scratch pool's pooled takes, misses (no free slot of
+// the stream or unowned) and takeovers (a completed armed slot of another
+// stream) since the context was created
+extern "C" __attribute__((visibility("default"))) int priskv_crc_cov_pool(const priskv_crc_ctx *ctx, uint64_t *out)
+{
+    if (!ctx || !out)
+        return -EINVAL;
+    pthread_mutex_lock(&ctx->pool_lock);
+    out[0] = ctx->pool_calls;
+    out[1] = ctx->pool_misses;
+    out[2] = ctx->pool_takeovers;
+    pthread_mutex_unlock(&ctx->pool_lock);
+    return 0;
+}
+#endif
+
 int priskv_crc_stream_release(const priskv_crc_ctx *ctx, void *stream)
 {
     if (!ctx)
@@ -1850,15 +1993,23 @@ int priskv_crc_stream_release(const priskv_crc_ctx *ctx, void *stream)
     if (!g.ok)
         return -ENODEV;
     const hipStream_t s = (hipStream_t)stream;
-    if (int rc = herr(hipStreamSynchronize(s))) // the slots' last uses
-        return rc;
-    const pthread_t self = pthread_self();
+    StreamKey key;
+    {
+        RelaxedCapture relaxed;
+        if (int rc = herr(hipStreamSynchronize(s))) // the slots' last uses
+            return rc;
+        if (!stream_key(s, &key))
+            return -EIO;
+        free_deferred(true);
+    }
     pthread_mutex_lock(&ctx->pool_lock);
     for (priskv_crc_pool_slot *slots : {ctx->pool, ctx->cnt_pool})
         for (int i = 0; i < NPOOL; i++) {
             priskv_crc_pool_slot &q = slots[i];
-            if (!q.busy && q.homed && q.home == s && (s != hipStreamPerThread || pthread_equal(q.tid, self)))
+            if (!q.busy && slot_owned_by(q, key)) {
                 q.homed = 0;
+                q.armed = 0;
+            }
         }
     pthread_mutex_unlock(&ctx->pool_lock);
     return 0;
@@ -1970,14 +2121,21 @@ namespace {
 // Is [h, h + len) one contiguous device-visible mapping (registered or
 // pinned)?  Both ends are looked up: a registration that ends inside the
 // range would otherwise pass as a mapping of all of it.
+// A lookup that fails (an unregistered range) sets the thread's last HIP
+// error; it is cleared again only if the caller had no error pending, so a
+// server's own earlier error stays visible to its hipGetLastError (HIP has no
+// call that restores a specific code: a pending one may read as
+// hipErrorInvalidValue afterwards, but it is not lost).
 bool host_mapped(const void *h, uint64_t len, void **dptr)
 {
     void *d0 = nullptr, *d1 = nullptr;
     const uint8_t *last = (const uint8_t *)h + len - 1;
+    const bool pending = hipPeekAtLastError() != hipSuccess;
     const bool ok = hipHostGetDevicePointer(&d0, const_cast<void *>(h), 0) == hipSuccess && d0 &&
                     hipHostGetDevicePointer(&d1, const_cast<uint8_t *>(last), 0) == hipSuccess && d1 &&
                     (uint8_t *)d1 - (uint8_t *)d0 == (ptrdiff_t)(len - 1);
-    (void)hipGetLastError();
+    if (!pending)
+        (void)hipGetLastError();
     *dptr = ok ? d0 : nullptr;
     return ok;
 }

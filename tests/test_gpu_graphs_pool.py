@@ -301,8 +301,10 @@ def test_streams_created_and_destroyed_per_connection(torch_cuda, ctx):
     """A server that creates a stream per connection: 20 streams, more than
     the pool's slots, each created, used for split-mode and fused calls, and
     destroyed -- half of them after priskv_crc_stream_release, half without
-    (their slots return through the idle-stream takeover, which queries
-    destroyed handles).  Every CRC exact, then two live streams at once."""
+    (their slots stay out of use: the pool was not contended when they were
+    last released, so no event marks their end, and later streams fall back
+    to per-call allocation).  Every CRC exact, then two live streams at once.
+    The contended and in-flight cases: tests/test_gpu_pool_contention.py."""
     torch = torch_cuda
     hip = _hip()
     region = 64 * MIB

@@ -1749,14 +1749,18 @@ def test_window_blocks_deep_plan(torch_cuda, ctx, bs, shift, nb, kernel):
 
 
 @pytest.mark.slow
-def test_stride_kernel_beyond_4GiB(torch_cuda, ctx):
-    """1.1 M blocks of 4100 B (4.5 GB, group pointers past 2^32) on an
-    odd base: sampled blocks (first, last, every 4096th) against the oracle,
-    and the batch equals the same batch run as two halves."""
+@pytest.mark.parametrize("bs,nb,mis,kind", [(4607, 1000000, 1, "crc_stride_kernel<"),
+                                             (4100, 1100000, 5, "window")])
+def test_stride_and_window_beyond_4GiB(torch_cuda, ctx, bs, nb, mis, kind):
+    """Batches past 4 GiB on odd bases, so group pointers pass 2^32: 4607-B
+    blocks (the stride kernel) and 4100-B blocks (window mode since round 5):
+    sampled blocks (first, last, every 4096th) against the oracle, and the
+    batch equals the same batch run as two halves."""
     torch = torch_cuda
-    bs, nb, mis = 4100, 1100000, 5
-    t = _region(torch, ctx, bs * nb + 16, SEED ^ 0x4100, 0)
+    t = _region(torch, ctx, bs * nb + 16, SEED ^ bs, 0)
     view = t[mis: mis + bs * nb]
+    plan = ctx.blocks_plan(view.data_ptr(), nb, bs)
+    assert kind in plan, plan
     got = ctx.blocks_dev(view, bs, nblocks=nb)
     idx = np.unique(np.concatenate([np.arange(0, nb, 4096), [nb - 1]])).astype(np.int64)
     blocks = view.view(nb, bs).index_select(0, torch.from_numpy(idx).cuda()).cpu().numpy()

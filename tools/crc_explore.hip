@@ -311,7 +311,7 @@ static uint32_t *g_nib[65] = {};
                const uint32_t *fold, uint32_t *o) {                                                            \
                 hipLaunchKernelGGL((crc_rows_kernel<G, CH, NB, 2, OPT>), g, dim3(kThreads), 0, s, b, n, bs, img,   \
                                    ((OPT) & 32) ? g_nib[G] : fold, o, (uint32_t)(((WE) << 16) | (WO)), 0u, bs, 1u, \
-                                   nullptr, nullptr, nullptr);                                                 \
+                                   nullptr, (uint64_t *)nullptr);                                              \
             }, {}}
 // oversubscribed: K workgroups per CU in the grid, 32 KiB of dynamic LDS on
 // top of the 64 KiB tables so only ONE is resident per CU -- the hardware
