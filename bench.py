@@ -107,6 +107,8 @@ def parse(argv=None):
     p.add_argument("--no-streamed", action="store_true", help="skip the configs[4] (host-resident) leg")
     p.add_argument("--no-odd", action="store_true", help="skip the odd block size legs (4095 / 4097 B)")
     p.add_argument("--streamed-steps", type=int, default=5)
+    p.add_argument("--detail", default=None,
+                   help="where the full result goes (default gpurun_out/bench_detail.json); stdout gets the compact line")
     return p.parse_args(argv)
 
 
@@ -227,26 +229,30 @@ def launch_stats(ms):
             "max_ms": round(float(a.max()), 4)}
 
 
-def read_roof(B, region, bs, nb, stream, alg, k):
+def read_roof(B, region, bs, nb, stream, alg, k, rotate=0):
     """The measured peak beside the CRC's roofline: priskv_crc_read_roof_dev
     (the CRC kernel's loads, per-wave ranges and XCD split, no hashing) over
     the same region in every variant -- the CRC plan's own pipeline depth and
     occupancy, and 2 / 3 / 4 chunks in flight at one or two workgroups per CU
-    -- ramped like the CRC, k launches each with one event pair per launch.
-    measured_peak is the best variant's mean rate: a roof of the pattern, not
-    one sibling kernel's rate.  GB/s of the same algorithmic bytes."""
+    -- each ramped the same way, in an order rotated by `rotate` (so no
+    variant always runs first or last), k launches each with one event pair
+    per launch.  measured_peak is the best variant's mean rate (a roof of the
+    pattern, not one sibling kernel's rate); measured_peak_v0, variant 0's
+    alone (the CRC plan's own shape: the round-3 roof, comparable across
+    rounds).  GB/s of the same algorithmic bytes."""
     from priskv_amd.crc import ROOF_SINK_WORDS, ROOF_VARIANTS
     torch = B.torch
     sink = torch.zeros(ROOF_SINK_WORDS, dtype=torch.int32, device=B.dev)
     per = {}
-    for v in range(ROOF_VARIANTS):
+    order = [(v + rotate) % ROOF_VARIANTS for v in range(ROOF_VARIANTS)]
+    for v in order:
         def step():
             B.ctx.read_roof_dev(region, bs, sink, stream=stream, nblocks=nb, variant=v)
 
         step()
         torch.cuda.synchronize()
-        # the device is in its steady state after the CRC leg: a short ramp per variant
-        ramp(step, stream, torch, window=8, min_s=0.05 if v else 0.3, max_s=2.0)
+        # the device is in its steady state after the CRC leg: the same short ramp for every variant
+        ramp(step, stream, torch, window=8, min_s=0.15, max_s=2.0)
         ms = per_launch_ms(step, stream, torch, k)
         per[v] = (float(np.mean(ms)), launch_stats(ms))
     del sink
@@ -255,13 +261,15 @@ def read_roof(B, region, bs, nb, stream, alg, k):
     return {"measured_peak": round(alg / (mean * 1e-3) / 1e9, 1),
             "measured_peak_best": round(alg / (st["min_ms"] * 1e-3) / 1e9, 1),
             "measured_peak_variant": best,
-            "measured_peak_variants_GBps": {str(v): round(alg / (per[v][0] * 1e-3) / 1e9, 1) for v in per},
+            "measured_peak_v0": round(alg / (per[0][0] * 1e-3) / 1e9, 1),
+            "measured_peak_variants_GBps": {str(v): round(alg / (per[v][0] * 1e-3) / 1e9, 1) for v in sorted(per)},
+            "measured_peak_order": order,
             "measured_peak_source": "priskv_crc_read_roof_dev on the same region in this process: the CRC kernel's "
                                     "loads, per-wave ranges and XCD split without hashing, best of "
                                     f"{ROOF_VARIANTS} variants (variant 0 = the CRC plan's own pipeline depth and "
                                     "occupancy; 1-6 = 2/2/3/3/4/4 chunks in flight at 1/2 workgroups per CU; 7-8 = "
-                                    "the plan's shape with progress priority 1/3); "
-                                    f"mean of {k} launches each (one event pair per launch) after a ramp",
+                                    "the plan's shape with progress priority 1/3), each ramped alike, order rotated "
+                                    f"per leg; mean of {k} launches each (one event pair per launch)",
             "roof_launch_ms": st}
 
 
@@ -319,7 +327,7 @@ class Bench:
         return region, None
 
 
-def resident_leg(B: Bench, name, steps, parity="full"):
+def resident_leg(B: Bench, name, steps, parity="full", rotate=0):
     """A device-resident config (CONFIGS[name]) at this N: each rank's shard
     of world x nb blocks, filled on the device, ramped, then `steps` timed
     passes.  parity "full": every block of every shard against the oracle;
@@ -347,7 +355,7 @@ def resident_leg(B: Bench, name, steps, parity="full"):
     el, kms = B.timed(step, stream, k)
     alg = nb * (bs + 4)
     lstats = launch_stats(per_launch_ms(step, stream, torch, k))
-    roof = read_roof(B, region, bs, nb, stream, alg, k) if bs % 4096 == 0 else None
+    roof = read_roof(B, region, bs, nb, stream, alg, k, rotate) if bs % 4096 == 0 else None
     if parity == "full":
         host = region.cpu().numpy()
         got = as_u32(out)
@@ -372,6 +380,7 @@ def resident_leg(B: Bench, name, steps, parity="full"):
     if roof:
         rl.update(roof)
         rl["frac_of_measured"] = round(achieved / roof["measured_peak"], 4)
+        rl["frac_of_v0"] = round(achieved / roof["measured_peak_v0"], 4)
     return {"workload": desc, "value": round(bs * nb * B.world * k / el / 2**30, 2), "unit": "GiB/s",
             "n_gpus": B.world, "steps": k, "ms_per_step": round(el / k * 1e3, 4), "bytes_per_gpu": bs * nb,
             "kernel": plan, "roofline": rl,
@@ -490,6 +499,84 @@ def cpu_model():
     return "unknown"
 
 
+def _r(x, nd=4):
+    return None if x is None else round(float(x), nd)
+
+
+def compact_leg(leg: dict) -> dict:
+    """One leg of the stdout line: value, ms_per_step, frac, frac_of_measured,
+    traffic (measured HBM bytes / algorithmic bytes), bit_exact (or the
+    leg's error / skip reason)."""
+    if not isinstance(leg, dict):
+        return {"error": str(leg)}
+    if "error" in leg or "skipped" in leg:
+        return {k: leg[k] for k in ("error", "skipped") if k in leg}
+    rl = leg.get("roofline") or {}
+    tr = rl.get("traffic")
+    alg = rl.get("alg_bytes_per_launch")
+    out = {"value": leg.get("value"), "ms_per_step": leg.get("ms_per_step"), "frac": rl.get("frac"),
+           "frac_of_measured": rl.get("frac_of_measured"),
+           "traffic": _r(tr / alg) if tr and alg else None,
+           "bit_exact": (leg.get("parity") or {}).get("bit_exact")}
+    return {k: v for k, v in out.items() if v is not None or k in ("traffic", "frac_of_measured")}
+
+
+def compact_line(full: dict, detail_path: str) -> dict:
+    """The ONE stdout line: the contract's keys, the headline roofline and
+    cpu_baseline in short form, and every other leg as compact_leg -- short
+    enough (~2.5 KB) that a driver keeping the last 3000 characters of stdout
+    sees every leg.  Everything else (per-variant roofs, per-launch stats,
+    sources, notes, per-rank identity) is in the detail file."""
+    rl = full.get("roofline", {})
+    line = {k: full[k] for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
+                                 "higher_is_better", "scaling", "vs_baseline", "dtype", "data") if k in full}
+    cfg = full.get("config", {})
+    line["config"] = {k: cfg[k] for k in ("workload", "block_size", "nblocks_per_gpu", "parallelism", "kernel")
+                      if k in cfg}
+    line["roofline"] = {k: rl[k] for k in ("bound", "achieved", "peak", "unit", "frac", "traffic", "kernel_ms",
+                                           "measured_peak", "measured_peak_v0", "frac_of_measured", "frac_of_v0")
+                        if k in rl}
+    if "cpu_baseline" in full:
+        cb = full["cpu_baseline"]
+        line["cpu_baseline"] = {k: cb[k] for k in ("value", "unit", "cores", "kind") if k in cb}
+        line["cpu_baseline"]["sample"] = (cb.get("sample", "").split(";")[0] + "; server/crc.c -O2 (oracle/_ref), "
+                                          f"1 thread on {cb.get('cpu', '?')}")
+        mt = [v for v in cb.get("variants", []) if v.get("opt") == "-O2" and v.get("threads", 1) > 1]
+        if mt:
+            line["cpu_baseline"]["multithread"] = {"threads": mt[0]["threads"], "value": mt[0]["value"]}
+    par = full.get("parity", {})
+    line["parity"] = {k: par[k] for k in ("bit_exact", "bit_exact_vs_reference_build", "checked_blocks_per_rank")
+                      if k in par}
+    d = full.get("dist", {})
+    line["dist"] = {k: d[k] for k in ("backend", "world_size", "distinct_devices", "rehearsal") if k in d}
+    legs = {}
+    for k, v in (full.get("sweep") or {}).items():
+        legs[k] = compact_leg(v)
+    if "tib" in full:
+        legs["tib"] = compact_leg(full["tib"])
+    for k, v in (full.get("odd") or {}).items():
+        legs[f"odd{k}"] = compact_leg(v)
+    st = full.get("streamed")
+    if isinstance(st, dict):
+        for mode in ("pinned", "pageable"):
+            if mode in st:
+                m = st[mode]
+                legs[f"streamed_{mode}"] = {"value": m.get("value"), "ms_per_step": m.get("ms_per_step"),
+                                            "frac": (m.get("roofline") or {}).get("frac"),
+                                            "bit_exact": m.get("bit_exact")}
+        if "error" in st:
+            legs["streamed"] = {"error": st["error"]}
+    cold = full.get("cold")
+    if isinstance(cold, dict):
+        legs["cold"] = ({"value": cold.get("value"), "ms": cold.get("ms"), "frac": cold.get("frac"),
+                         "walked_value": cold.get("walked_value")} if "error" not in cold else {"error": cold["error"]})
+    line["legs"] = legs
+    if "cold_ms" in full:
+        line["cold_ms"] = full["cold_ms"]
+    line["detail"] = detail_path
+    return line
+
+
 def main():
     global T_START
     T_START = time.perf_counter()
@@ -606,6 +693,7 @@ def main():
     if roof:
         result["roofline"].update(roof)
         result["roofline"]["frac_of_measured"] = round(achieved / roof["measured_peak"], 4)
+        result["roofline"]["frac_of_v0"] = round(achieved / roof["measured_peak_v0"], 4)
 
     # the whole shard to host (untimed): every block is checked against the
     # oracle, rank 0's first cpu-sample-bytes time the CPU baseline, and the
@@ -643,9 +731,10 @@ def main():
             progress(rank, f"{label} done in {walls[label]:.1f} s")
 
     if not args.no_sweep and args.config == "default":
-        result["sweep"] = {k: leg(f"sweep_{k}", resident_leg, B, name, args.sweep_steps) for k, name in SWEEP}
+        result["sweep"] = {k: leg(f"sweep_{k}", resident_leg, B, name, args.sweep_steps, rotate=1 + i)
+                           for i, (k, name) in enumerate(SWEEP)}
     if not args.no_tib and args.config == "default":
-        result["tib"] = leg("tib", resident_leg, B, "tib", args.tib_steps, parity="sampled")
+        result["tib"] = leg("tib", resident_leg, B, "tib", args.tib_steps, parity="sampled", rotate=3)
     if not args.no_odd and args.config == "default":
         result["odd"] = {k: leg(f"odd_{k}", resident_leg, B, name, args.sweep_steps, parity="sampled")
                          for k, name in ODD}
@@ -682,7 +771,15 @@ def main():
         result["leg_wall_s"] = {k: round(v, 2) for k, v in walls.items()}
         result["leg_wall_s"]["note"] = ("rank 0's wall seconds per leg (process start to the line); the legs "
                                         "open and close with barriers, so rank 0's time is the job's")
-        print(json.dumps(result), flush=True)
+        detail = args.detail or os.path.join(ROOT, "gpurun_out", "bench_detail.json")
+        try:
+            os.makedirs(os.path.dirname(os.path.abspath(detail)), exist_ok=True)
+            with open(detail, "w") as f:
+                json.dump(result, f, indent=1)
+        except OSError as e:
+            detail = f"not written: {e}"
+        print(json.dumps(compact_line(result, os.path.relpath(detail, ROOT) if os.path.isabs(detail) else detail)),
+              flush=True)
     if world > 1:
         dist.destroy_process_group()
 
