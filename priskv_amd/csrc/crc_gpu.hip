@@ -66,6 +66,7 @@ struct priskv_crc_pool_slot {
     int homed;               // home is set (the slot has been taken once)
     int busy;                // taken by a call in flight on the host
     int armed;               // ev was recorded after the slot's last use (pool contended)
+    int plain;               // p came from hipMalloc (scratch_alloc), not the stream-ordered pool
     hipEvent_t ev;           // the library's own event (created on first need)
 };
 
@@ -270,6 +271,43 @@ void free_deferred(bool force)
     (void)hipThreadExchangeStreamCaptureMode(&mode);
 }
 
+// queue a buffer for free_deferred (its hipFree synchronises the device
+// first, so every use of the buffer is complete by then)
+void defer_free(void *p, int device, size_t bytes)
+{
+    DeferredFree *d = new (std::nothrow) DeferredFree{p, device, bytes ? bytes : 4};
+    if (d)
+        graph_scratch_release(d); // (leaks p if even that allocation fails)
+}
+
+// Stream-ordered scratch.  While any blocking stream is being captured, HIP
+// refuses hipMallocAsync / hipFreeAsync on every stream, relaxed capture mode
+// or not (hipErrorStreamCaptureUnsupported; round 6,
+// tools/capture_blocking_probe.py); then the call takes a plain hipMalloc
+// (the caller is in relaxed mode) and frees it through the deferred queue.
+int scratch_alloc(void **p, size_t bytes, hipStream_t s, int *plain)
+{
+    *plain = 0;
+    const hipError_t e = hipMallocAsync(p, bytes, s);
+    if (e == hipSuccess)
+        return 0;
+    if (e == hipErrorOutOfMemory)
+        return -ENOMEM;
+    if (hipMalloc(p, bytes) != hipSuccess)
+        return herr(e);
+    *plain = 1;
+    return 0;
+}
+
+void scratch_free(void *p, int plain, size_t bytes, hipStream_t s, int device)
+{
+    if (!p)
+        return;
+    if (!plain && hipFreeAsync(p, s) == hipSuccess)
+        return;
+    defer_free(p, device, bytes);
+}
+
 int graph_scratch(const priskv_crc_ctx *ctx, hipStream_t s, size_t bytes, void **out)
 {
     hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
@@ -375,6 +413,8 @@ struct Scratch {
     bool zero;
     int slot = -1;
     void *p = nullptr;
+    int plain = 0;    // (slot < 0) p came from hipMalloc
+    size_t nbytes = 0;
     Scratch(const priskv_crc_ctx *c, hipStream_t st) : ctx(c), s(st), slots(c->pool), zero(false) {}
     Scratch(const priskv_crc_ctx *c, hipStream_t st, priskv_crc_pool_slot *pool_slots, bool zeroed)
         : ctx(c), s(st), slots(pool_slots), zero(zeroed)
@@ -453,11 +493,11 @@ struct Scratch {
                     size_t cap = 64u << 10;
                     while (cap < bytes)
                         cap *= 2;
-                    if (q.p) // after the slot's last use: same stream, or a completed armed event
-                        rc = herr(hipFreeAsync(q.p, s));
+                    // after the slot's last use: same stream, or a completed armed event
+                    scratch_free(q.p, q.plain, q.size, s, ctx->device);
                     q.p = nullptr;
                     q.size = 0;
-                    if (!rc && !(rc = herr(hipMallocAsync(&q.p, cap, s))))
+                    if (!(rc = scratch_alloc(&q.p, cap, s, &q.plain)))
                         q.size = cap;
                     if (!rc && zero && (rc = zero_fill(q.p, cap)))
                         q.size = 0; // not known zero: the next user reallocates (and frees q.p)
@@ -473,7 +513,8 @@ struct Scratch {
                 return 0;
             }
         }
-        int rc = herr(hipMallocAsync(&p, bytes, s));
+        nbytes = bytes;
+        int rc = scratch_alloc(&p, bytes, s, &plain);
         if (!rc && zero)
             rc = zero_fill(p, bytes);
         return rc;
@@ -485,7 +526,9 @@ struct Scratch {
             return 0;
         if (slot < 0) {
             RelaxedCapture relaxed;
-            return p ? herr(hipFreeAsync(p, s)) : 0;
+            scratch_free(p, plain, nbytes, s, ctx->device);
+            p = nullptr;
+            return 0;
         }
         priskv_crc_pool_slot &q = slots[slot];
         pthread_mutex_lock(&ctx->pool_lock);
@@ -1929,7 +1972,9 @@ void priskv_crc_ctx_destroy(priskv_crc_ctx *c)
             (void)hipDeviceSynchronize();
         for (priskv_crc_pool_slot *slots : {c->pool, c->cnt_pool})
             for (int i = 0; i < NPOOL; i++) {
-                if (slots[i].p)
+                if (slots[i].p && slots[i].plain)
+                    (void)hipFree(slots[i].p);
+                else if (slots[i].p)
                     (void)hipFreeAsync(slots[i].p, c->aux);
                 if (slots[i].ev)
                     (void)hipEventDestroy(slots[i].ev);

@@ -135,9 +135,12 @@ def _fill(torch, t, seed):
         torch.cuda.synchronize()
 
 
-def _new_stream(hip):
+def _new_stream(hip, nonblocking=False):
     s = ctypes.c_void_p()
-    assert hip.hipStreamCreate(ctypes.byref(s)) == 0
+    if nonblocking:  # hipStreamNonBlocking: no implicit ordering with the legacy default stream
+        assert hip.hipStreamCreateWithFlags(ctypes.byref(s), 1) == 0
+    else:
+        assert hip.hipStreamCreate(ctypes.byref(s)) == 0
     return s
 
 
@@ -201,7 +204,8 @@ def test_destroyed_stream_in_flight_then_contended_pool(torch_cuda, build):
         R.close()
 
 
-def test_capture_on_one_thread_while_another_exhausts_pool(torch_cuda):
+@pytest.mark.parametrize("kind", ["blocking", "nonblocking"])
+def test_capture_on_one_thread_while_another_exhausts_pool(torch_cuda, kind):
     """stream X homes a pool slot; thread A begins a
     global-mode capture on X and captures split and fused calls; meanwhile
     thread B drives 9 other streams through split and fused calls until the
@@ -226,10 +230,16 @@ def test_capture_on_one_thread_while_another_exhausts_pool(torch_cuda):
               torch.full((5,), -1, dtype=torch.int32, device="cuda"))
         ob = [(torch.full((4,), -1, dtype=torch.int32, device="cuda"),
                torch.full((5,), -1, dtype=torch.int32, device="cuda")) for _ in range(NPOOL + 1)]
-        X = _new_stream(hip)
+        # blocking streams (hipStreamCreate): while a blocking stream is being
+        # captured HIP refuses hipMallocAsync / hipFreeAsync on every stream,
+        # so B's calls that need new scratch take the library's plain-malloc
+        # fallback (tools/capture_blocking_probe.py)
+        nb = kind == "nonblocking"
+        X = _new_stream(hip, nonblocking=nb)
         R.blocks(t, 16 * MIB, 4, oa[0], X.value)  # X homes a slot
         assert hip.hipStreamSynchronize(X) == 0
-        bs = [_new_stream(hip) for _ in range(NPOOL + 1)]
+        bs = [_new_stream(hip, nonblocking=nb) for _ in range(NPOOL + 1)]
+
         torch.cuda.synchronize()
         # no torch call below until both threads are done: torch's allocator
         # would itself be an illegal call under A's global-mode capture
@@ -251,6 +261,14 @@ def test_capture_on_one_thread_while_another_exhausts_pool(torch_cuda):
 
         def thread_b():
             try:
+                # B's own stream synchronisations below would be illegal under
+                # A's global-mode capture (hipErrorStreamCaptureUnsupported,
+                # and they invalidate A's capture): B runs in relaxed mode, as
+                # a server thread beside a capturing one must.  The library's
+                # own calls do not depend on it (its pool calls switch to
+                # relaxed mode themselves): tools/capture_blocking_probe.py.
+                mode = ctypes.c_int(2)  # hipStreamCaptureModeRelaxed
+                assert hip.hipThreadExchangeStreamCaptureMode(ctypes.byref(mode)) == 0
                 began.wait(60)
                 for rnd in range(4):
                     for s, o in zip(bs, ob):
@@ -366,7 +384,7 @@ def test_xcd_split_coverage(torch_cuda):
             outs = [torch.full((n,), -1, dtype=torch.int32, device="cuda") for _ in streams]
             plans[name] = wt.plan(t, n, bs)
             assert "xcd-weighted" not in fb.plan(t, n, bs), (name, fb.plan(t, n, bs))
-            torch.cuda.synchronize()
+            wt.cov_take()  # (the counters are one per library: drop the previous case's fallback calls)
             wt.blocks(t, bs, n, outs[0], streams[0].cuda_stream)
             N, idx = wt.cov_take()  # synchronises the device
             assert N > 0 and (ng is None or N == ng), (name, N, ng)
