@@ -231,7 +231,10 @@ int priskv_crc32_blocks_plan(const priskv_crc_ctx *ctx, const void *d_base, uint
 /* Diagnostic: the read roof of the CRC kernel's access pattern.  Reads
  * nblocks x block_size bytes at d_base with the loads, per-wave ranges and
  * XCD split crc_rows_kernel uses for this block size (block_size a multiple
- * of 4 KiB, d_base 16-byte aligned), without hashing.  variant 0 runs in the
+ * of 4 KiB, d_base 16-byte aligned), without hashing.  For an odd block size
+ * that the window mode hashes with 4 KiB-multiple windows (4095, 4097, 4100 B
+ * ...; priskv_crc32_blocks_path 7) it reads every block's window -- the
+ * W bytes ending at the 16-byte boundary at or after the block's end.  variant 0 runs in the
  * CRC plan's own pipeline depth and occupancy; variants 1 ..
  * 6 in 2, 2, 3, 3, 4, 4 chunks in flight at one / two 8-wave workgroups per
  * CU, variants 7 and 8 in the plan's shape with the CRC kernels' progress

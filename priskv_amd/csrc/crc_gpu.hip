@@ -1726,9 +1726,18 @@ int priskv_crc32_blocks_plan(const priskv_crc_ctx *ctx, const void *d_base, uint
 int priskv_crc_read_roof_dev(const priskv_crc_ctx *ctx, const void *d_base, uint64_t nblocks, uint32_t block_size,
                              uint32_t variant, uint32_t *d_sink, void *stream)
 {
-    if (!ctx || block_size == 0 || block_size % 4096 != 0 || ((uintptr_t)d_base & 15) != 0 ||
-        variant >= PRISKV_CRC_ROOF_VARIANTS)
+    if (!ctx || block_size == 0 || ((uintptr_t)d_base & 15) != 0 || variant >= PRISKV_CRC_ROOF_VARIANTS)
         return -EINVAL;
+    // an odd block size the window mode takes with a 4 KiB-multiple window:
+    // the roof reads the windows (crc_read_roof_kernel stride)
+    uint32_t stride = 0;
+    if (block_size % 4096 != 0) {
+        const uint32_t W = window_bytes(ctx, d_base, nblocks, block_size);
+        if (!W || W % 4096 != 0)
+            return -EINVAL;
+        stride = block_size;
+        block_size = W;
+    }
     if (nblocks == 0)
         return 0;
     if (!d_base || !d_sink)
@@ -1743,7 +1752,9 @@ int priskv_crc_read_roof_dev(const priskv_crc_ctx *ctx, const void *d_base, uint
     // launch_plan applies them); the roof reads units as blocks
     int p = plan_for(block_size, nblocks);
     uint32_t S = 1;
-    if (segments_for(ctx, nblocks, block_size) == 1)
+    if (stride) // (launch_window: the W plan, whole blocks, no tiles)
+        ;
+    else if (segments_for(ctx, nblocks, block_size) == 1)
         S = split_for(ctx, nblocks, block_size);
     else if ((S = split_few(ctx, nblocks, block_size)) > 1)
         p = PLAN_SPLIT_DEEP;
@@ -1763,7 +1774,7 @@ int priskv_crc_read_roof_dev(const priskv_crc_ctx *ctx, const void *d_base, uint
     const uint8_t *b = static_cast<const uint8_t *>(d_base);
     uint32_t bs = block_size;
     uint32_t xw = nblocks >= 32ull * grid * kWaves ? ctx->plan_xw[p] : 0u;
-    uint32_t tile = S == 1 ? tile_groups(ctx, nblocks, bs) : 0u; // the CRC kernel's tiles (G = 64: a group is a block)
+    uint32_t tile = S == 1 && !stride ? tile_groups(ctx, nblocks, bs) : 0u; // the CRC kernel's tiles (G = 64: a group is a block)
     if (tile)
         xw = 0;
     const void *fn = nbuf == 4   ? (prio == 1   ? reinterpret_cast<const void *>(&crc_read_roof_kernel<4, 4, kAux, 1>)
@@ -1775,7 +1786,8 @@ int priskv_crc_read_roof_dev(const priskv_crc_ctx *ctx, const void *d_base, uint
                                  : (prio == 1   ? reinterpret_cast<const void *>(&crc_read_roof_kernel<4, 2, kAux, 1>)
                                     : prio == 3 ? reinterpret_cast<const void *>(&crc_read_roof_kernel<4, 2, kAux, 3>)
                                                 : reinterpret_cast<const void *>(&crc_read_roof_kernel<4, 2, kAux>));
-    void *args[] = {(void *)&b, (void *)&nblocks, (void *)&bs, (void *)&d_sink, (void *)&xw, (void *)&tile};
+    void *args[] = {(void *)&b, (void *)&nblocks, (void *)&bs, (void *)&d_sink, (void *)&xw, (void *)&tile,
+                    (void *)&stride};
     return herr(hipLaunchKernel(fn, dim3(grid), dim3(kThreads), args, 0, (hipStream_t)stream));
 }
 

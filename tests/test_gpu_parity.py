@@ -390,8 +390,9 @@ def test_read_roof_dev(torch_cuda, ctx):
     plans bench.py measures (4 KiB, 64 KiB, 1 MiB incl. the split mode, few
     large blocks); each launched wave stores the XOR of its words in its own
     sink slot, so the XOR of the zeroed sink equals the XOR of the whole
-    region's 32-bit words; it refuses what it cannot mirror (block sizes not
-    multiples of 4 KiB, unaligned bases, unknown variants)."""
+    region's 32-bit words; odd sizes of the window mode read their 4 KiB
+    windows; it refuses what it cannot mirror (other block sizes, unaligned
+    bases, unknown variants)."""
     import errno
     from priskv_amd.crc import ROOF_SINK_WORDS, ROOF_VARIANTS
     torch = torch_cuda
@@ -418,8 +419,23 @@ def test_read_roof_dev(torch_cuda, ctx):
             assert got == want, ("tiles", bs, hex(got), hex(want))
     finally:
         tiles.close()
+    # odd sizes the window mode takes (4 KiB windows): the roof reads each
+    # block's window, the 4096 bytes ending at the 16-B boundary at or after
+    # the block's end, so the sink's XOR is the XOR of those windows' words
+    host = t[:256 << 20].cpu().numpy()
+    for bs in (4095, 4097, 4100, 4111):
+        nb = 30000
+        ends = ((np.arange(1, nb + 1, dtype=np.int64) * bs + 15) // 16) * 16
+        idx = (ends[:, None] - 4096 + np.arange(0, 4096, 4)[None, :]).reshape(-1)
+        wwant = int(np.bitwise_xor.reduce(host[idx[:, None] + np.arange(4)].reshape(-1).view(np.uint32)))
+        for v in range(ROOF_VARIANTS):
+            sink.zero_()
+            ctx.read_roof_dev(t, bs, sink, nblocks=nb, variant=v)
+            torch.cuda.synchronize()
+            got = int(np.bitwise_xor.reduce(sink.cpu().numpy().view(np.uint32)))
+            assert got == wwant, ("window", bs, v, hex(got), hex(wwant))
     from priskv_amd.crc import lib
-    for bs, off, v in ((1024, 0, 0), (4100, 0, 0), (4096, 4, 0), (4096, 0, ROOF_VARIANTS)):
+    for bs, off, v in ((1024, 0, 0), (5000, 0, 0), (4096, 4, 0), (4096, 0, ROOF_VARIANTS), (4095, 4, 0)):
         assert lib().priskv_crc_read_roof_dev(ctx.handle, t[off:].data_ptr(), 4, bs, v, sink.data_ptr(),
                                               None) == -errno.EINVAL
     with pytest.raises(ValueError):
