@@ -47,6 +47,14 @@ def load(spec):
 
 libs = {a: load(a) for a in ARGS}
 TAGS = list(libs)
+# each context's plan for the headline shape (its XCD probe result shows as
+# "xcd-weighted" or not): a context whose probe found no round-robin dispatch
+# runs equal shares, which differs by a percent or two
+for _tag, (_L, _h) in libs.items():
+    _L.priskv_crc32_blocks_plan.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint32, C.c_char_p, C.c_uint64]
+    _buf = C.create_string_buffer(256)
+    _L.priskv_crc32_blocks_plan(_h, C.c_void_p(1 << 20), 1 << 20, 4096, _buf, 256)
+    print(json.dumps({"variant": _tag, "plan_1Mix4KiB": _buf.value.decode()}), flush=True)
 STREAMS = [torch.cuda.Stream() for _ in range(NSTREAMS)]
 s = STREAMS[0]
 region = torch.empty(4 << 30, dtype=torch.uint8, device="cuda")
