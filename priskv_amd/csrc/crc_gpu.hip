@@ -731,11 +731,7 @@ constexpr Plan kPlans[NPLANS] = {
     {16, 4, 2, kPrio1, 1, 31, 29},          {64, 4, 2, kPrio1, 1, 31, 29},      {64, 4, 2, kPrio3, 1, 31, 29},
     {64, 2, 2, 0, 1, 31, 29},               {64, 1, 2, 0, 1, 31, 29},
     {64, 4, 3, kEarly | 32 | kPrio3, 1, 31, 29}, // (4 deep: 1 x 256 MiB +1.8 %, 16 x 16 MiB +3.2 % slower, profiles/r04/split/split_deep_nbuf4_ab.jsonl)
-#ifdef PRISKV_CRC_DIAG_PAIR4K // A/B build: the deep 4 KiB plan with chains (PRISKV_CRC_DIAG_CHAINS), PAIR4K deep
-    {64, 4, PRISKV_CRC_DIAG_PAIR4K, 2 | kEarly | 32 | kPrio3 | PRISKV_CRC_DIAG_CHAINS, 1, 31, 29}};
-#else
     {64, 4, 4, 2 | kEarly | 32 | kPrio3, 1, 31, 29}};
-#endif
 
 // 4 KiB blocks in batches of at least this many: four chunks in flight
 // instead of three, +0.4-0.5 % at 4 GiB on every one of 6 allocations on two
@@ -1233,7 +1229,7 @@ int launch_head_split(const priskv_crc_ctx *ctx, const uint8_t *base, uint64_t n
 constexpr uint32_t kWinMaxBytes = 16u << 10, kWinOver = 48;
 constexpr uint32_t kStrideMax = 9u << 10; // the stride / extents kernels' boundary (stride_to_extents)
 constexpr int kWinImages = (int)(kWinMaxBytes / 1024);
-constexpr int kWinOpt = 8192, kChainOpts = 16384 | 32768;
+constexpr int kWinOpt = 8192;
 
 uint32_t window_bytes(const priskv_crc_ctx *ctx, const void *base, uint64_t nblocks, uint32_t bs)
 {
@@ -1266,7 +1262,7 @@ const void *window_kernel_p()
 {
     constexpr Plan Q = kPlans[P];
     static_assert(!(Q.opt & 1024), "window mode: 8-wave workgroups");
-    return plan_kernel<Q.G, Q.CH, Q.NBUF, (Q.opt & ~kChainOpts) | kWinOpt>(); // (chains: not in windows)
+    return plan_kernel<Q.G, Q.CH, Q.NBUF, Q.opt | kWinOpt>();
 }
 
 // the window kernel of W's plan: G = 64 for multiples of 4 KiB, G = 16 (four
