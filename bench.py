@@ -534,11 +534,11 @@ def compact_line(full: dict, detail_path: str) -> dict:
     line = {k: full[k] for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
                                  "higher_is_better", "scaling", "vs_baseline", "dtype", "data") if k in full}
     cfg = full.get("config", {})
-    line["config"] = {k: cfg[k] for k in ("workload", "block_size", "nblocks_per_gpu", "parallelism", "kernel")
-                      if k in cfg}
+    line["config"] = {k: cfg[k] for k in ("workload", "block_size", "nblocks_per_gpu", "parallelism", "kernel",
+                                          "timed_launches") if k in cfg}
     line["roofline"] = {k: rl[k] for k in ("bound", "achieved", "peak", "unit", "frac", "traffic", "kernel_ms",
-                                           "measured_peak", "measured_peak_v0", "frac_of_measured", "frac_of_v0")
-                        if k in rl}
+                                           "alg_bytes_per_launch", "measured_peak", "measured_peak_v0",
+                                           "frac_of_measured", "frac_of_v0") if k in rl}
     if "cpu_baseline" in full:
         cb = full["cpu_baseline"]
         line["cpu_baseline"] = {k: cb[k] for k in ("value", "unit", "cores", "kind") if k in cb}

@@ -52,7 +52,8 @@ def blocks_case(ctx, bs, total, steps=10):
     sec = timeit(lambda: ctx.blocks_dev(t, bs, out=out), steps)
     samp = min(nb, max(1, (256 << 20) // bs))
     ok = np.array_equal(as_u32(out[:samp]), O.crc32_blocks(t[: samp * bs].cpu().numpy(), bs, nthreads=16))
-    emit(path="blocks_dev", kernel=blocks_path(t.data_ptr(), nb, bs), block_size=bs, nblocks=nb,
+    emit(path="blocks_dev", kernel=blocks_path(t.data_ptr(), nb, bs), plan=ctx.blocks_plan(t.data_ptr(), nb, bs)[:90],
+         block_size=bs, nblocks=nb,
          ms=round(sec * 1e3, 4), GiBs=round(nb * bs / sec / 2**30, 1), TBs=round(nb * (bs + 4) / sec / 1e12, 3),
          checked=samp, bit_exact=bool(ok))
     del t, out
@@ -258,6 +259,10 @@ def main():
     if "paths1g" in which:  # DESIGN §6 "Other paths": 1 GiB per call, every non-headline block plan
         for bs in (4096, 4096, 16, 32, 64, 128, 256, 512, 100, 1000, 1023, 2047, 4095, 4097, 4100, 12345, 65537):
             blocks_case(ctx, bs, 1 << 30)
+    if "paths4g" in which:  # the same plans at the headline's ~4 GiB per call (fixed costs out of the way)
+        for bs in (4096, 4096, 16, 32, 64, 128, 256, 512, 100, 1000, 1023, 1025, 2047, 2049, 4095, 4097, 4100,
+                   8193, 12345, 65537):
+            blocks_case(ctx, bs, 4 << 30)
     if "ranges" in which:
         ranges_dev_case(ctx)
         ranges_dev_case(ctx, bs=65536, n=1 << 15)

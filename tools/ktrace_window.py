@@ -3,10 +3,10 @@
 
 usage: ktrace_window.py BENCH_JSON KTRACE_DIR
 
-BENCH_JSON is bench.py's stdout (the one JSON line) of a run made under
+BENCH_JSON is bench.py's stdout (the one JSON line) or its detail file of a run made under
 `rocprofv3 --kernel-trace --stats -d KTRACE_DIR`.  The headline kernel is the
-crc_rows_kernel instance with the most dispatches (warmup + ramp + timed
-steps); the line's config.timed_launches names which of its dispatches were
+crc_rows_kernel instance dispatched first (warmup + ramp + timed steps come
+before every other leg); the line's config.timed_launches names which of its dispatches were
 the K timed steps (they follow the W warmup and the untimed ramp).  Prints
 one JSON object: mean / median / min / max duration of exactly those K
 dispatches, the roofline fraction each gives (algorithmic bytes per launch /
@@ -25,7 +25,11 @@ from collections import defaultdict
 def main():
     line = None
     with open(sys.argv[1]) as f:
-        for ln in f:
+        text = f.read()
+    try:  # bench.py's detail file (gpurun_out/bench_detail.json): one JSON document
+        line = json.loads(text)
+    except ValueError:  # its stdout: the JSON line among other output
+        for ln in text.splitlines():
             ln = ln.strip()
             if ln.startswith("{"):
                 line = json.loads(ln)
@@ -39,7 +43,9 @@ def main():
             if "crc_rows_kernel" in r["Kernel_Name"]:
                 by_name[r["Kernel_Name"]].append((int(r["Dispatch_Id"]), int(r["End_Timestamp"]) -
                                                   int(r["Start_Timestamp"])))
-    name = max(by_name, key=lambda k: len(by_name[k]))
+    # the headline is the first rows kernel the process dispatched (the odd
+    # legs' window kernels may have more dispatches in all)
+    name = min(by_name, key=lambda k: min(i for i, _ in by_name[k]))
     d = [t for _, t in sorted(by_name[name])]
     win = d[lo - 1:hi]
     if len(win) != hi - lo + 1:
