@@ -730,11 +730,7 @@ constexpr Plan kPlans[NPLANS] = {
     {64, 4, 3, 2 | kEarly | 32 | kPrio3, 1, 31, 29}, {64, 4, 2, 32 | kPrio1, 1, 31, 29}, {16, 4, 2, 2 | 32 | kPrio1, 1, 31, 29},
     {16, 4, 2, kPrio1, 1, 31, 29},          {64, 4, 2, kPrio1, 1, 31, 29},      {64, 4, 2, kPrio3, 1, 31, 29},
     {64, 2, 2, 0, 1, 31, 29},               {64, 1, 2, 0, 1, 31, 29},
-#ifdef PRISKV_CRC_PIPE_SPLIT // A/B: the split mode on the pipelined fold (per-chunk CRCs joined by Horner's rule)
-    {64, 4, 3, 2 | kEarly | 32 | kPrio3, 1, 31, 29},
-#else
     {64, 4, 3, kEarly | 32 | kPrio3, 1, 31, 29}, // (4 deep: 1 x 256 MiB +1.8 %, 16 x 16 MiB +3.2 % slower, profiles/r04/split/split_deep_nbuf4_ab.jsonl)
-#endif
     {64, 4, 4, 2 | kEarly | 32 | kPrio3, 1, 31, 29}};
 
 // 4 KiB blocks in batches of at least this many: four chunks in flight
@@ -778,7 +774,7 @@ template <int P>
 const void *plan_kernel_p(bool split)
 {
     constexpr Plan Q = kPlans[P];
-    if constexpr (plan_splits(P) || P == PLAN_SPLIT_DEEP) {
+    if constexpr (plan_splits(P)) {
         // the few-large-blocks plan merges its parts per workgroup (a lone
         // block has a part in every wave; per-wave atomics elsewhere: the
         // workgroup barrier cost 2 % on 4 Ki x 1 MiB, profiles/r04/split/)
