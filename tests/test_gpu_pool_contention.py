@@ -412,3 +412,62 @@ def test_xcd_split_coverage(torch_cuda):
     finally:
         for R in (wt, fb):
             R.close()
+
+
+def test_per_thread_streams_contend_for_the_pool(torch_cuda):
+    """More host threads on hipStreamPerThread than pool slots: with the HIP
+    runtime PyTorch ships (no hipStreamGetId) each thread's slot is keyed by
+    (handle, thread), so 12 threads contend for 8 slots, arm their releases
+    and may take over each other's completed slots.  Every CRC exact; the
+    coverage build must report misses; then every thread's slots go back
+    through priskv_crc_stream_release on that thread."""
+    torch = torch_cuda
+    hip = _hip()
+    R = Raw(COV_SO)
+    HIP_STREAM_PER_THREAD = 2
+    try:
+        region = 64 * MIB
+        t = torch.empty(region, dtype=torch.uint8, device="cuda")
+        _fill(torch, t, 0x7E4D)
+        offs, lens = _extents(4, region, 8 * MIB, 41)
+        d_o = torch.from_numpy(offs.astype(np.int64)).cuda()
+        d_l = torch.from_numpy(lens.view(np.int32)).cuda()
+        host = t.cpu().numpy()
+        want_b = O.crc32_blocks(host, 16 * MIB, nthreads=8)
+        want_r = O.crc32_ranges(host, offs, lens)
+        nthreads = NPOOL + 4
+        outs = [(torch.full((4,), -1, dtype=torch.int32, device="cuda"),
+                 torch.full((4,), -1, dtype=torch.int32, device="cuda")) for _ in range(nthreads)]
+        torch.cuda.synchronize()
+        errors, results = [], {}
+        barrier = threading.Barrier(nthreads)
+
+        def worker(i):
+            try:
+                for it in range(4):
+                    for _ in range(2):
+                        R.blocks(t, 16 * MIB, 4, outs[i][0], HIP_STREAM_PER_THREAD)
+                        R.ranges(t, d_o, d_l, outs[i][1], HIP_STREAM_PER_THREAD)
+                    assert hip.hipStreamSynchronize(ctypes.c_void_p(HIP_STREAM_PER_THREAD)) == 0
+                    results[(i, it)] = (_u32(outs[i][0]).copy(), _u32(outs[i][1]).copy())
+                    barrier.wait(timeout=60)
+                assert R.L.priskv_crc_stream_release(R.h, HIP_STREAM_PER_THREAD) == 0
+            except Exception as e:  # noqa: BLE001
+                errors.append((i, repr(e)))
+                barrier.abort()
+
+        th = [threading.Thread(target=worker, args=(i,)) for i in range(nthreads)]
+        for x in th:
+            x.start()
+        for x in th:
+            x.join(timeout=120)
+        assert not errors, errors
+        assert len(results) == nthreads * 4
+        for (i, it), (b, r) in results.items():
+            assert np.array_equal(b, want_b), (i, it)
+            assert np.array_equal(r, want_r), (i, it)
+        st = R.cov_pool()
+        print("pool:", st)
+        assert st["misses"] > 0, st  # (takeovers depend on the threads' timing; test (a) forces one)
+    finally:
+        R.close()
