@@ -426,7 +426,7 @@ struct Scratch {
         const uint32_t grid = (uint32_t)(nw / 256 + 1 < 1024 ? nw / 256 + 1 : 1024);
         return launch_k(crc_zero_kernel, dim3(grid), dim3(256), s, static_cast<uint32_t *>(q), nw);
     }
-    // a free slot for stream id sid (pool_lock held), or -1
+    // a free slot for the stream with this key (pool_lock held), or -1
     int pick(const StreamKey &key, size_t bytes) const
     {
         // free slots of this stream first, then unowned ones: the smallest
