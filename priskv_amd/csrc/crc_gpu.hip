@@ -2026,6 +2026,19 @@ extern "C" __attribute__((visibility("default"))) int priskv_crc_cov_take(const 
     return 0;
 }
 
+// test-only build: the per-wave timing records of the last rows-kernel
+// launches (g_wave_t: n <= 8192 records of 4 words), after the device is idle
+extern "C" __attribute__((visibility("default"))) int priskv_crc_cov_waves(const priskv_crc_ctx *ctx, uint64_t *out,
+                                                                          uint64_t n)
+{
+    if (!ctx || !out || n > (uint64_t)kCovWaves)
+        return -EINVAL;
+    DevGuard g(ctx->device);
+    if (int rc = herr(hipDeviceSynchronize()))
+        return rc;
+    return herr(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wave_t), n * 4 * sizeof(uint64_t)));
+}
+
 // test-only build: the scratch pool's pooled takes, misses (no free slot of
 // the stream or unowned) and takeovers (a completed armed slot of another
 // stream) since the context was created
