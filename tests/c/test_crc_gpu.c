@@ -10,7 +10,8 @@
  * restatement of server/crc.c:90-109, loaded with dlopen: a checker, not
  * linked into anything the product ships).
  *
- *   blocks_dev    4 KiB / 64 KiB / 1 MiB / 4100-B / 256-B blocks, on a stream
+ *   blocks_dev    4 KiB / 64 KiB / 1 MiB / 4100-B / 256-B blocks, and 4 and 1 large
+ *                 blocks (split across workgroups), on a stream
  *   ranges_dev    PrisKV-shaped values (value_off on a 4 KiB block, valuelen ragged)
  *   verify_dev    the same values, clean and with one corrupted byte
  *   ranges_host   the zero-copy memfile scrub over a registered host region
@@ -100,7 +101,9 @@ int main(void)
     /* ---- blocks_dev */
     {
         const int before = failures;
-        static const uint32_t sizes[] = {4096, 65536, 1u << 20, 4100, 256};
+        /* (REGION / 4 and REGION: few large blocks, whose parts finish
+         * across workgroups through the zero-at-rest word) */
+        static const uint32_t sizes[] = {4096, 65536, 1u << 20, 4100, 256, REGION / 4, REGION};
         uint32_t *d_out, *h_out = malloc(sizeof(uint32_t) * (REGION / 256));
         HIPOK(hipMalloc((void **)&d_out, sizeof(uint32_t) * (REGION / 256)));
         for (size_t k = 0; k < sizeof(sizes) / sizeof(sizes[0]); k++) {
@@ -123,7 +126,7 @@ int main(void)
         }
         HIPOK(hipFree(d_out));
         free(h_out);
-        report("blocks_dev 4 KiB / 64 KiB / 1 MiB / 4100 B / 256 B", before);
+        report("blocks_dev 4 KiB / 64 KiB / 1 MiB / 4100 B / 256 B / 4 and 1 large blocks", before);
     }
 
     /* PrisKV-shaped values: start on a 4 KiB block, occupy 1/2/4 blocks, ragged length */
