@@ -471,3 +471,73 @@ def test_per_thread_streams_contend_for_the_pool(torch_cuda):
         assert st["misses"] > 0, st  # (takeovers depend on the threads' timing; test (a) forces one)
     finally:
         R.close()
+
+
+def test_mixed_paths_soak_many_threads(torch_cuda):
+    """A short soak: 6 host threads on two contexts, each thread creating a
+    stream per round (half of them destroyed without release or sync) and
+    issuing the paths that draw pooled scratch -- split few large blocks,
+    the balanced split, fused values -- beside plain rows, window and
+    sub-KiB calls, on one read-only region; more live streams than slots.
+    Every result against the oracle."""
+    torch = torch_cuda
+    hip = _hip()
+    ctxs = [Raw(PROD_SO), Raw(PROD_SO)]
+    try:
+        region = 192 * MIB
+        t = torch.empty(region, dtype=torch.uint8, device="cuda")
+        _fill(torch, t, 0x50A4)
+        offs, lens = _extents(5, 64 * MIB, 12 * MIB, 51)
+        d_o = torch.from_numpy(offs.astype(np.int64)).cuda()
+        d_l = torch.from_numpy(lens.view(np.int32)).cuda()
+        host = t.cpu().numpy()
+        # (block size, blocks): few large (split few), balanced 1 MiB split,
+        # 4 KiB rows, 4095-B window, 256-B sub-KiB
+        shapes = [(16 * MIB, 4), (MIB, 190), (4096, 40000), (4095, 40000), (256, 200000)]
+        want = {bs: O.crc32_blocks(host[: bs * nb], bs, nthreads=16) for bs, nb in shapes}
+        want_r = O.crc32_ranges(host[: 64 * MIB], offs, lens)
+        nthreads, rounds = 6, 5
+        outs = [{bs: torch.full((nb,), -1, dtype=torch.int32, device="cuda") for bs, nb in shapes}
+                for _ in range(nthreads)]
+        routs = [torch.full((5,), -1, dtype=torch.int32, device="cuda") for _ in range(nthreads)]
+        torch.cuda.synchronize()
+        errors, bad = [], []
+
+        def worker(i):
+            try:
+                R = ctxs[i % 2]
+                for r in range(rounds):
+                    st = _new_stream(hip, nonblocking=bool((i + r) % 2))
+                    for bs, nb in shapes:
+                        R.blocks(t, bs, nb, outs[i][bs], st.value)
+                    R.ranges(t, d_o, d_l, routs[i], st.value)
+                    assert hip.hipStreamSynchronize(st) == 0
+                    for bs, nb in shapes:
+                        if not np.array_equal(_u32(outs[i][bs]), want[bs]):
+                            bad.append((i, r, bs))
+                    if not np.array_equal(_u32(routs[i]), want_r):
+                        bad.append((i, r, "ranges"))
+                    # the next round's calls on this thread's next stream; this
+                    # one destroyed -- released first on even rounds only
+                    if r % 2 == 0:
+                        assert R.L.priskv_crc_stream_release(R.h, st.value) == 0
+                    for bs, nb in shapes:
+                        R.blocks(t, bs, nb, outs[i][bs], st.value)  # in flight at the destroy
+                    assert hip.hipStreamDestroy(st) == 0
+                    assert hip.hipDeviceSynchronize() == 0
+                    for bs, nb in shapes:
+                        if not np.array_equal(_u32(outs[i][bs]), want[bs]):
+                            bad.append((i, r, bs, "after destroy"))
+            except Exception as e:  # noqa: BLE001
+                errors.append((i, repr(e)))
+
+        th = [threading.Thread(target=worker, args=(i,)) for i in range(nthreads)]
+        for x in th:
+            x.start()
+        for x in th:
+            x.join(timeout=300)
+        assert not errors, errors
+        assert not bad, bad[:10]
+    finally:
+        for R in ctxs:
+            R.close()
