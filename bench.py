@@ -12,9 +12,14 @@ its own 4 GiB shard -- the next 1 Mi blocks of one global region -- and
 checksums it with no data-path collective ("weak" scaling); the barrier and
 the max-over-ranks reduction are the benchmark contract, not part of the path.
 
-Extra keys of the ONE JSON line rank 0 prints (every BASELINE config that
-fits a GPU is measured in the same run, each timed outside the headline's
-timed region, with barrier + max over ranks at N > 1):
+Rank 0 prints ONE compact JSON line (~2.5 KB, compact_line: the contract's
+keys, the headline roofline and cpu_baseline, and under "legs" each other
+leg's value, ms_per_step, frac, frac_of_measured, traffic ratio and
+bit_exact) and writes the full result below to the detail file
+(gpurun_out/bench_detail.json, --detail).  The legs of the full result
+(every BASELINE config that fits a GPU is measured in the same run, each
+timed outside the headline's timed region, with barrier + max over ranks at
+N > 1):
   sweep         configs[2]: 64 Ki x 64 KiB and 4 Ki x 1 MiB (4 GiB per GPU
                 each), device-resident, each with its kernel's roofline and
                 every block checked bit-exactly against the CPU oracle
@@ -23,7 +28,9 @@ timed region, with barrier + max over ranks at N > 1):
                 (first, last, every 4096th block of every shard)
   odd           1 M x 4095 B and 1 M x 4097 B blocks per rank (odd sizes the
                 server's -v accepts; the rows kernel's window mode), sampled
-                parity, traffic from profiles/ when measured
+                parity, the window pattern's read roof, traffic from
+                profiles/ when measured; run before tib (a region allocated
+                after the 128 GiB leg reads slower)
   streamed      configs[4]: the headline's 1 Mi x 4 KiB blocks from HOST
                 memory, end to end (H2D copies, kernels and D2H of the CRCs
                 overlapped on 3 streams, priskv_crc32_blocks_host): pinned
