@@ -1003,7 +1003,6 @@ constexpr uint32_t kSegMinLen = 64u << 10;
 constexpr int kFusedPrio = 0;
 constexpr uint64_t kFusedUnitsPerWave = 32; // with XCD weights (fused_xw)
 constexpr uint32_t kFusedMinShift = 10;     // ... segments of at least 1 KiB
-constexpr uint64_t kFusedFewExtents = 16;   // the 8-wave shape up to this many extents
 
 // one segment size per call (crc_seg_plan_kernel / the fused kernel): about
 // kSegPerWave full segments per resident wave, so the count split of
@@ -1045,23 +1044,22 @@ int launch_fused(const priskv_crc_ctx *ctx, const uint8_t *base, uint64_t n, con
     // XCD weights (fused_xw): segments of >= 1 KiB, about kFusedUnitsPerWave per
     // resident wave, so that the weights (whole units) apply to large calls;
     // else about kSegPerWave of >= 16 KiB (round 3)
-    // Shape: 16 waves per CU with 2-row chunks 2 deep; for at most
-    // kFusedFewExtents extents -- a lone large value, a few: the ones with
-    // the most bytes per wave -- 8 waves with 4-row chunks 2 deep (the 64 KiB
-    // rows plan's), which stream 4-8 % faster there but lose 7 % at 32 x 1 MiB
-    // (profiles/r04/fused/shape_ab.jsonl; 8 x 2 x 2 and 8 x 4 x 3 lost).
-    const bool few = n <= kFusedFewExtents;
-    const int nw = few ? 8 : kFusedWaves;
+    // Shape: 16 waves per CU with 2-row chunks 2 deep, whatever the count.
+    // Rounds 4-5 ran at most 16 extents -- a lone large value, a few -- on 8
+    // waves with 4-row chunks, which streamed 4-8 % faster there
+    // (profiles/r04/fused/shape_ab.jsonl).  With round 6's one-word finish
+    // the 16-wave shape (and its finer segment target) came out 1-2 % faster
+    // for those calls too: 1 x 256 MiB 53.4 -> 52.3 us, 4 x 64 MiB 52.1 ->
+    // 51.1, 16 x 2 MiB 14.5 -> 14.4, medians of 12 in one process
+    // (profiles/r06/fused/fused_16w_ab.jsonl).
+    const int nw = kFusedWaves;
     const uint64_t waves = (uint64_t)ctx->num_cus * nw;
     const uint64_t want = kFusedUnitsPerWave * waves;
     const uint32_t tgt = 1u << (31 - __builtin_clz((uint32_t)std::min<uint64_t>(want, 1u << 30))); // a power of two
     uint32_t ms = kFusedMinShift;
     uint32_t xw = ctx->plan_xw[PLAN_4K];
     // (16 waves: 4- and 8-row chunks lost 6-13 % on a lone 256 MiB value, profiles/r03/fused/)
-    // (8 waves: progress priority, 3-deep 4-row and 2-deep 8-row chunks all level, profiles/r04/fused/prio_depth_ab.jsonl)
-    const void *fn =
-        few ? reinterpret_cast<const void *>(&crc_ranges_fused_kernel<4, kNbuf, kAux, kFusedPrio, 8>)
-            : reinterpret_cast<const void *>(&crc_ranges_fused_kernel<kExtRows, kNbuf, kAux, kFusedPrio, kFusedWaves>);
+    const void *fn = reinterpret_cast<const void *>(&crc_ranges_fused_kernel<kExtRows, kNbuf, kAux, kFusedPrio, kFusedWaves>);
     const uint32_t *img = ctx->d_lds_image[0], *nib = ctx->d_nib16, *rs = ctx->d_rowshift, *zp = ctx->d_zpow;
     void *args[] = {(void *)&abase, (void *)&n,   (void *)&offs, (void *)&lens_or_null, (void *)&sh,
                     (void *)&stride, (void *)&len_const, (void *)&img, (void *)&nib, (void *)&rs,

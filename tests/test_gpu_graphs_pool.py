@@ -80,8 +80,9 @@ def _dev(torch, offs, lens):
     return (torch.from_numpy(offs.astype(np.int64)).cuda(), torch.from_numpy(lens.view(np.int32)).cuda())
 
 
-# (name, extents, longest extent): the fused kernel's three plan shapes -- the
-# 8-wave shape up to 16 extents, the wave plan up to 64, the LDS prefix above
+# (name, extents, longest extent): the fused kernel's plans -- the wave plan
+# up to 64 extents (a few large ones, and many smaller), the LDS prefix above
+# (rounds 4-5 also ran an 8-wave shape up to 16 extents; round 6 dropped it)
 _FUSED_SHAPES = [("fused<=16", 3, 24 * MIB), ("fused17-64", 40, 2 * MIB), ("fused>64", 300, 512 << 10)]
 
 
