@@ -1593,6 +1593,59 @@ def test_fused_few_extents(torch_cuda, ctx_fused16k, ctx_threelaunch, case):
     assert np.array_equal(got, want)
 
 
+_MANY_WG_CASES = [
+    ("blocks", [48 << 20] * 5),                   # blocks straddling groups of 16 workgroups, XCD-weighted units
+    ("blocks", [32 << 20] * 7),
+    ("blocks", [256 << 20]),                      # every group shares the lone block
+    ("ranges", [40 << 20, (3 << 20) + 5, 100 << 20, 1024, (77 << 20) + 1]),
+    ("ranges", [(9 << 20) + 3] * 11),
+    ("ranges", [256 << 20]),
+]
+
+
+def test_many_workgroup_finish(torch_cuda, ctx):
+    """finish_shared (crc_device.inc) for items shared by many workgroups:
+    blocks / values across groups of workgroups (partial at both ends), and
+    lone items with a share in every workgroup, on the merging split plan and
+    the fused kernel's wave plan.  Each call three times back to back and
+    interleaved with the other shapes (the zero-at-rest words must be left
+    zero), every CRC against the oracle.  (Round 6 also ran these cases on a
+    two-level finish through per-group words, tools/patches/finish_two_level.patch:
+    exact, and 0.3-0.5 us slower per call, so not kept.)"""
+    torch = torch_cuda
+    total = max(sum(ls) + 64 * len(ls) for _, ls in _MANY_WG_CASES) + 4096
+    t = _region(torch, ctx, total + 5, SEED ^ 0x2F1, 1)
+    host = t[:total + 5].cpu().numpy()
+    rng = np.random.default_rng(77)
+    calls = []
+    for kind, ls in _MANY_WG_CASES:
+        lens = np.array(ls, dtype=np.uint32)
+        if kind == "blocks":
+            bs, nb = int(lens[0]), len(lens)
+            assert "few large blocks" in ctx.blocks_plan(t.data_ptr(), nb, bs)  # the merging split plan
+            want = O.crc32_blocks(host[:bs * nb], bs, nthreads=16)
+            calls.append((lambda bs=bs, nb=nb: ctx.blocks_dev(t, bs, nblocks=nb), want))
+        else:
+            offs, pos = [], 5
+            for ln in lens:
+                pos += int(rng.integers(0, 64))
+                offs.append(pos)
+                pos += int(ln)
+            o = np.array(offs, dtype=np.uint64)
+            d_o = torch.from_numpy(o.astype(np.int64)).cuda()
+            d_l = torch.from_numpy(lens.view(np.int32)).cuda()
+            want = O.crc32_ranges(host, o, lens)
+            calls.append((lambda d_o=d_o, d_l=d_l: ctx.ranges_dev(t, d_o, d_l), want))
+    for rnd in range(2):
+        order = list(range(len(calls))) if rnd == 0 else list(reversed(range(len(calls))))
+        for i in order:
+            fn, want = calls[i]
+            for _ in range(3):
+                got = _u32(fn())
+                torch.cuda.synchronize()
+                assert np.array_equal(got, want), (_MANY_WG_CASES[i], np.nonzero(got != want)[0][:8])
+
+
 @pytest.mark.parametrize("bs,nb", [((3 << 20) + 5, 3), (4100 * 64, 17), ((1 << 24) + 1, 1)])
 def test_fused_constant_length_blocks(torch_cuda, ctx, bs, nb):
     """Blocks that are not whole 1 KiB rows (the extents path with one length
