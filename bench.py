@@ -114,6 +114,9 @@ def parse(argv=None):
     p.add_argument("--no-streamed", action="store_true", help="skip the configs[4] (host-resident) leg")
     p.add_argument("--no-odd", action="store_true", help="skip the odd block size legs (4095 / 4097 B)")
     p.add_argument("--streamed-steps", type=int, default=5)
+    p.add_argument("--fresh-regions", action="store_true",
+                   help="the 4 GiB legs (64 KiB, 1 MiB, odd sizes) each allocate their own region instead of "
+                        "re-filling the headline's (rounds 1-6)")
     p.add_argument("--detail", default=None,
                    help="where the full result goes (default gpurun_out/bench_detail.json); stdout gets the compact line")
     return p.parse_args(argv)
@@ -334,20 +337,31 @@ class Bench:
         return region, None
 
 
-def resident_leg(B: Bench, name, steps, parity="full", rotate=0):
+def resident_leg(B: Bench, name, steps, parity="full", rotate=0, shared=None):
     """A device-resident config (CONFIGS[name]) at this N: each rank's shard
     of world x nb blocks, filled on the device, ramped, then `steps` timed
     passes.  parity "full": every block of every shard against the oracle;
-    "sampled": first, last and every 4096th block."""
+    "sampled": first, last and every 4096th block.  shared: the headline's
+    region, which the leg's blocks go into (re-filled with the leg's own
+    pattern) when they fit -- one value region, as PrisKV's values live in
+    one registered memfile region -- so that the legs do not each draw a fresh
+    4 GiB allocation, whose read rate differs by a few percent from one
+    allocation to the next; the leg's read roof is measured on
+    the same region either way."""
     import _oracle as O
     from priskv_amd import as_u32
     from priskv_amd.shard import shard_blocks, shard_word_offset
     torch, ctx = B.torch, B.ctx
     bs, nb0, desc = CONFIGS[name]
     first, nb = shard_blocks(B.world * nb0, B.rank, B.world)
-    region, err = B.alloc(bs * nb)
-    if region is None:
-        return {"workload": desc, "skipped": f"cannot allocate {bs * nb / 2**30:.0f} GiB: {err}"}
+    # (every rank's shard has the same size, so every rank takes the same branch)
+    if shared is not None and shared.numel() >= bs * nb:
+        region, where = shared[: bs * nb], "the headline's region (shared)"
+    else:
+        region, err = B.alloc(bs * nb)
+        if region is None:
+            return {"workload": desc, "skipped": f"cannot allocate {bs * nb / 2**30:.0f} GiB: {err}"}
+        where = "its own allocation"
     ctx.fill_splitmix(region, SEED, word_offset=shard_word_offset(first, bs))
     out = torch.empty(nb, dtype=torch.int32, device=B.dev)
     stream = torch.cuda.Stream(device=B.dev)
@@ -393,7 +407,7 @@ def resident_leg(B: Bench, name, steps, parity="full", rotate=0):
         rl["frac_of_v0"] = round(achieved / roof["measured_peak_v0"], 4)
     return {"workload": desc, "value": round(bs * nb * B.world * k / el / 2**30, 2), "unit": "GiB/s",
             "n_gpus": B.world, "steps": k, "ms_per_step": round(el / k * 1e3, 4), "bytes_per_gpu": bs * nb,
-            "kernel": plan, "roofline": rl,
+            "region": where, "kernel": plan, "roofline": rl,
             "parity": {"checked_blocks_per_rank": nchk, "sample": what, "bit_exact": ok,
                        "oracle": "oracle/crc_oracle.c"}}
 
@@ -716,6 +730,7 @@ def main():
     walls["parity"] = time.perf_counter() - t_leg
     progress(rank, f"headline {value:.1f} GiB/s, parity {'ok' if head_ok else 'FAILED'}")
     walked = region if args.config == "default" else None
+    shared = None if args.fresh_regions else walked  # the 4 GiB legs' blocks go into this region
     if walked is None:
         del region
     del out
@@ -741,14 +756,15 @@ def main():
             progress(rank, f"{label} done in {walls[label]:.1f} s")
 
     if not args.no_sweep and args.config == "default":
-        result["sweep"] = {k: leg(f"sweep_{k}", resident_leg, B, name, args.sweep_steps, rotate=1 + i)
+        result["sweep"] = {k: leg(f"sweep_{k}", resident_leg, B, name, args.sweep_steps, rotate=1 + i, shared=shared)
                            for i, (k, name) in enumerate(SWEEP)}
     # the odd sizes before the 128 GiB leg: a region allocated after that
     # leg's free read 5-6 % slower, its read roof too (0.78 against 0.83 on one
     # box, profiles/r06/odd/): the state the benchmark's own largest leg
     # leaves, not the kernel
     if not args.no_odd and args.config == "default":
-        result["odd"] = {k: leg(f"odd_{k}", resident_leg, B, name, args.sweep_steps, parity="sampled", rotate=4 + i)
+        result["odd"] = {k: leg(f"odd_{k}", resident_leg, B, name, args.sweep_steps, parity="sampled", rotate=4 + i,
+                                shared=shared)
                          for i, (k, name) in enumerate(ODD)}
     if not args.no_tib and args.config == "default":
         result["tib"] = leg("tib", resident_leg, B, "tib", args.tib_steps, parity="sampled", rotate=3)
@@ -761,7 +777,7 @@ def main():
         result["cold"] = leg("cold", cold_leg, B, bs, nb, walked)
         if "ms" in result["cold"]:
             result["cold_ms"] = result["cold"]["ms"]
-        del walked
+        del walked, shared
     torch.cuda.empty_cache()
 
     kms = gather_obj(round(kernel_ms, 4), world)
