@@ -95,7 +95,12 @@ CASES = [("ranges 1x256MiB", 1, 256 << 20, 0), ("ranges 32x1MiB", 32, 1 << 20, (
          ("mid ranges 100x1MiB", 100, 1 << 20, 1 << 20), ("mid blocks 100x1MiB", 100, 1 << 20, 0),
          ("mid ranges 1000x128KiB", 1000, 128 << 10, 128 << 10), ("mid blocks 1000x128KiB", 1000, 128 << 10, 0),
          ("mid ranges 200x512KiB", 200, 512 << 10, 512 << 10), ("mid blocks 200x512KiB", 200, 512 << 10, 0),
-         ("mid ranges 1500x64KiB", 1500, 65536, 65536), ("mid blocks 1500x64KiB", 1500, 65536, 0)]
+         ("mid ranges 1500x64KiB", 1500, 65536, 65536), ("mid blocks 1500x64KiB", 1500, 65536, 0),
+         # tiny calls: launch and table-load latency (the fused kernel's wave plan up to 64 values)
+         ("tiny ranges 1x4KiB", 1, 4096, 4096), ("tiny ranges 16x4KiB", 16, 4096, 4096),
+         ("tiny ranges 64x4KiB", 64, 4096, 4096), ("tiny ranges 16x64KiB", 16, 65536, 65536),
+         ("tiny ranges 64x64KiB", 64, 65536, 65536), ("tiny blocks 1x4KiB", 1, 4096, 0),
+         ("tiny blocks 64x64KiB", 64, 65536, 0)]
 # PrisKV-shaped scattered values (tools/values_bench.py extents(): 1-4 blocks,
 # ragged ends, random blocks of the region)
 import numpy as np  # noqa: E402
