@@ -98,6 +98,18 @@ int priskv_crc32_ranges_dev(const priskv_crc_ctx *ctx, const void *d_base,
                             const uint64_t *d_offsets, const uint32_t *d_lengths, uint64_t n,
                             uint32_t *d_out, void *stream);
 
+/* priskv_crc32_ranges_dev with max_len, an upper bound on every d_lengths[i]
+ * that the caller knows on the host (the server holds each valuelen there,
+ * server/memory.h:50-51; 0 = unknown, which is priskv_crc32_ranges_dev).  A
+ * hint only: every result is exact whatever the lengths, but the launch is
+ * chosen from it -- values below 64 KiB are not segmented and the grid is
+ * sized by n, so a call of a few small values launches a few workgroups
+ * instead of the whole chip, and a bound of 64 KiB or more lets a balanced
+ * batch skip the segment plan. */
+int priskv_crc32_ranges_dev_bounded(const priskv_crc_ctx *ctx, const void *d_base,
+                                    const uint64_t *d_offsets, const uint32_t *d_lengths, uint64_t n,
+                                    uint64_t max_len, uint32_t *d_out, void *stream);
+
 /* Device-side verify of per-value extents (client-side integrity check):
  * compares priskv_crc32(d_base + d_offsets[i], d_lengths[i]) with
  * d_expected[i] for every i and writes d_status[0] = the number of values

@@ -47,6 +47,8 @@ SIGNATURES = [
      [_C.c_void_p, _C.c_void_p, _C.c_uint64, _C.c_uint32, _C.c_void_p, _C.c_void_p]),
     ("priskv_crc32_ranges_dev", _C.c_int,
      [_C.c_void_p, _C.c_void_p, _C.c_void_p, _C.c_void_p, _C.c_uint64, _C.c_void_p, _C.c_void_p]),
+    ("priskv_crc32_ranges_dev_bounded", _C.c_int,
+     [_C.c_void_p, _C.c_void_p, _C.c_void_p, _C.c_void_p, _C.c_uint64, _C.c_uint64, _C.c_void_p, _C.c_void_p]),
     ("priskv_crc32_verify_dev", _C.c_int,
      [_C.c_void_p, _C.c_void_p, _C.c_void_p, _C.c_void_p, _C.c_uint64, _C.c_void_p, _C.c_void_p, _C.c_void_p]),
     ("priskv_crc32_blocks_host", _C.c_int,
@@ -234,7 +236,9 @@ class CrcContext:
                                              _stream_ptr(stream)), "priskv_crc32_blocks_dev")
         return out
 
-    def ranges_dev(self, region, offsets, lengths, out=None, stream=None):
+    def ranges_dev(self, region, offsets, lengths, out=None, stream=None, max_len=None):
+        """priskv_crc32_ranges_dev; with max_len (a host-known upper bound on
+        the lengths, a launch hint only) priskv_crc32_ranges_dev_bounded."""
         import torch
         n = offsets.numel()
         if lengths.numel() != n or offsets.dtype != torch.int64 or lengths.dtype != torch.int32:
@@ -244,6 +248,12 @@ class CrcContext:
         if out.numel() < n or out.element_size() != 4:
             raise ValueError("out must be a 4-byte tensor of >= len(offsets) entries")
         _device_args(region, offsets, lengths, out)
+        if max_len is not None:
+            _check(lib().priskv_crc32_ranges_dev_bounded(self._h, region.data_ptr(), offsets.data_ptr(),
+                                                         lengths.data_ptr(), n, int(max_len), out.data_ptr(),
+                                                         _stream_ptr(stream)),
+                   "priskv_crc32_ranges_dev_bounded")
+            return out
         _check(lib().priskv_crc32_ranges_dev(self._h, region.data_ptr(), offsets.data_ptr(),
                                              lengths.data_ptr(), n, out.data_ptr(), _stream_ptr(stream)),
                "priskv_crc32_ranges_dev")

@@ -2121,6 +2121,16 @@ int priskv_crc32_ranges_dev(const priskv_crc_ctx *ctx, const void *d_base, const
     return ranges_dev(ctx, d_base, d_offsets, d_lengths, n, d_out, (hipStream_t)stream, 0);
 }
 
+// max_len only steers launch_extents' choice of kernel (every path hashes
+// any lengths exactly); lengths are u32, so larger bounds say nothing more
+int priskv_crc32_ranges_dev_bounded(const priskv_crc_ctx *ctx, const void *d_base, const uint64_t *d_offsets,
+                                    const uint32_t *d_lengths, uint64_t n, uint64_t max_len, uint32_t *d_out,
+                                    void *stream)
+{
+    return ranges_dev(ctx, d_base, d_offsets, d_lengths, n, d_out, (hipStream_t)stream,
+                      max_len < 0xFFFFFFFFull ? max_len : 0xFFFFFFFFull);
+}
+
 int priskv_crc32_verify_dev(const priskv_crc_ctx *ctx, const void *d_base, const uint64_t *d_offsets,
                             const uint32_t *d_lengths, uint64_t n, const uint32_t *d_expected,
                             uint64_t *d_status, void *stream)

@@ -159,19 +159,31 @@ int main(void)
         const int before = failures;
         uint32_t *got = malloc(sizeof(uint32_t) * NV);
         static const uint64_t counts[] = {NV, 20};
-        for (int c = 0; c < 2; c++) {
-            rc = priskv_crc32_ranges_dev(ctx, d_region, d_offs, d_lens, counts[c], d_crc, s);
+        uint32_t maxl = 0;
+        for (uint64_t i = 0; i < NV; i++)
+            maxl = lens[i] > maxl ? lens[i] : maxl;
+        /* c = 2, 3: the same through ranges_dev_bounded with the host-known
+         * longest length, and with a bound below it (a hint only: exact) */
+        for (int c = 0; c < 4; c++) {
+            const uint64_t cnt = counts[c & 1];
+            HIPOK(hipMemsetAsync(d_crc, 0xA5, sizeof(uint32_t) * cnt, s)); /* sentinel: every CRC is written */
+            if (c < 2)
+                rc = priskv_crc32_ranges_dev(ctx, d_region, d_offs, d_lens, cnt, d_crc, s);
+            else
+                rc = priskv_crc32_ranges_dev_bounded(ctx, d_region, d_offs, d_lens, cnt, c == 2 ? maxl : 16, d_crc,
+                                                     s);
             CHECK(rc == 0, "ranges_dev: %d", rc);
-            HIPOK(hipMemcpyAsync(got, d_crc, sizeof(uint32_t) * counts[c], hipMemcpyDeviceToHost, s));
+            HIPOK(hipMemcpyAsync(got, d_crc, sizeof(uint32_t) * cnt, hipMemcpyDeviceToHost, s));
             HIPOK(hipStreamSynchronize(s));
-            for (uint64_t i = 0; i < counts[c]; i++)
+            for (uint64_t i = 0; i < cnt; i++)
                 if (got[i] != want[i]) {
-                    CHECK(0, "ranges_dev n %llu value %llu", (unsigned long long)counts[c], (unsigned long long)i);
+                    CHECK(0, "ranges_dev%s n %llu value %llu", c < 2 ? "" : "_bounded", (unsigned long long)cnt,
+                          (unsigned long long)i);
                     break;
                 }
         }
         free(got);
-        report("ranges_dev PrisKV-shaped values", before);
+        report("ranges_dev / ranges_dev_bounded PrisKV-shaped values", before);
     }
 
     /* ---- verify_dev: clean, then one corrupted byte in value 1234 */

@@ -1646,6 +1646,50 @@ def test_many_workgroup_finish(torch_cuda, ctx):
                 assert np.array_equal(got, want), (_MANY_WG_CASES[i], np.nonzero(got != want)[0][:8])
 
 
+@pytest.mark.parametrize("case", ["tiny", "small_mixed", "wrong_bound", "large_bound", "huge_bound", "unknown"])
+def test_ranges_dev_bounded(torch_cuda, ctx, case):
+    """priskv_crc32_ranges_dev_bounded: max_len steers the launch only, so
+    every result equals the oracle whether the bound is tight, loose, wrong
+    (smaller than some lengths), beyond u32 or 0 (unknown); a 16-B-misaligned
+    base, zero lengths included, called twice."""
+    torch = torch_cuda
+    rng = np.random.default_rng(hash(case) & 0xFFFF)
+    if case == "tiny":
+        lens, bound = np.full(16, 4096, np.uint32), 4096
+    elif case == "small_mixed":
+        lens = rng.integers(0, 5000, 300).astype(np.uint32)
+        bound = int(lens.max())
+    elif case == "wrong_bound":  # the bound says 1 KiB, two values are MiBs
+        lens = rng.integers(0, 1024, 40).astype(np.uint32)
+        lens[[3, 17]] = [(1 << 20) + 7, 3 << 20]
+        bound = 1024
+    elif case == "large_bound":  # few large values: the segmented (fused) path
+        lens = np.array([(8 << 20) + 3, 0, 100, 5 << 20], np.uint32)
+        bound = int(lens.max())
+    elif case == "huge_bound":
+        lens = rng.integers(0, 70000, 100).astype(np.uint32)
+        bound = 1 << 40
+    else:
+        lens = rng.integers(0, 9000, 64).astype(np.uint32)
+        bound = 0
+    n = int(lens.sum()) + 64 * len(lens) + 4096
+    t = _region(torch, ctx, n + 3, SEED ^ 0xB0, 1)
+    base = t[3:]
+    offs, pos = [], 0
+    for ln in lens:
+        pos += int(rng.integers(0, 64))
+        offs.append(pos)
+        pos += int(ln)
+    o = np.array(offs, dtype=np.uint64)
+    d_o = torch.from_numpy(o.astype(np.int64)).cuda()
+    d_l = torch.from_numpy(lens.view(np.int32)).cuda()
+    want = O.crc32_ranges(base[:n].cpu().numpy(), o, lens)
+    for _ in range(2):
+        got = _u32(ctx.ranges_dev(base, d_o, d_l, max_len=bound))
+        torch.cuda.synchronize()
+        assert np.array_equal(got, want), (case, np.nonzero(got != want)[0][:8])
+
+
 @pytest.mark.parametrize("bs,nb", [((3 << 20) + 5, 3), (4100 * 64, 17), ((1 << 24) + 1, 1)])
 def test_fused_constant_length_blocks(torch_cuda, ctx, bs, nb):
     """Blocks that are not whole 1 KiB rows (the extents path with one length

@@ -27,6 +27,9 @@ def load(path):
     L.priskv_crc32_ranges_dev.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p,
                                           C.c_void_p]
     L.priskv_crc32_blocks_dev.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint32, C.c_void_p, C.c_void_p]
+    if hasattr(L, "priskv_crc32_ranges_dev_bounded"):  # (round 6 on)
+        L.priskv_crc32_ranges_dev_bounded.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64,
+                                                      C.c_uint64, C.c_void_p, C.c_void_p]
     h = C.c_void_p()
     assert L.priskv_crc_ctx_create(0, C.byref(h)) == 0
     return L, h
@@ -39,7 +42,10 @@ region = torch.empty(512 << 20, dtype=torch.uint8, device="cuda")
 region.random_(0, 256, generator=torch.Generator(device="cuda").manual_seed(3))
 big_out = torch.empty(1, dtype=torch.int32, device="cuda")
 CASES = [("ranges", 1, 4096), ("ranges", 16, 4096), ("ranges", 64, 4096), ("ranges", 16, 65536),
-         ("ranges", 64, 65536), ("ranges", 1, 1 << 20), ("blocks", 1, 4096), ("blocks", 64, 65536)]
+         ("ranges", 64, 65536), ("ranges", 1, 1 << 20), ("blocks", 1, 4096), ("blocks", 64, 65536),
+         # the same values with the host-known bound (priskv_crc32_ranges_dev_bounded, max_len = the length)
+         ("rangesb", 1, 4096), ("rangesb", 16, 4096), ("rangesb", 64, 4096), ("rangesb", 16, 65536),
+         ("rangesb", 64, 65536), ("rangesb", 1, 1 << 20)]
 ref = {}
 for r in range(ROUNDS):
     for ci, (kind, n, ln) in enumerate(CASES):
@@ -52,8 +58,14 @@ for r in range(ROUNDS):
             L, h = libs[tag]
             sp = s.cuda_stream
 
+            if kind == "rangesb" and not hasattr(L, "priskv_crc32_ranges_dev_bounded"):
+                continue
+
             def tiny():
-                if kind == "ranges":
+                if kind == "rangesb":
+                    rc = L.priskv_crc32_ranges_dev_bounded(h, region.data_ptr(), offs.data_ptr(), lens.data_ptr(), n,
+                                                           ln, out.data_ptr(), sp)
+                elif kind == "ranges":
                     rc = L.priskv_crc32_ranges_dev(h, region.data_ptr(), offs.data_ptr(), lens.data_ptr(), n,
                                                    out.data_ptr(), sp)
                 else:
@@ -76,7 +88,7 @@ for r in range(ROUNDS):
             us = [e0.elapsed_time(e1) * 1e3 for e0, e1 in ev]
             got = out.cpu().numpy().tobytes()
             name = f"{kind} {n}x{ln}"
-            assert ref.setdefault(name, got) == got, (name, tag)
+            assert ref.setdefault(name.replace("rangesb", "ranges"), got) == got, (name, tag)
             print(json.dumps({"round": r, "case": name, "variant": tag, "us_per_call": round(float(np.median(us)), 3),
                               "p10": round(float(np.percentile(us, 10)), 3),
                               "p90": round(float(np.percentile(us, 90)), 3)}), flush=True)
