@@ -123,6 +123,14 @@ int priskv_crc32_verify_dev(const priskv_crc_ctx *ctx, const void *d_base, const
                             const uint32_t *d_lengths, uint64_t n, const uint32_t *d_expected,
                             uint64_t *d_status, void *stream);
 
+/* priskv_crc32_verify_dev with max_len, a host-known upper bound on the
+ * lengths (0 = unknown): a launch hint only, exactly as
+ * priskv_crc32_ranges_dev_bounded's -- the status is exact whatever the
+ * lengths. */
+int priskv_crc32_verify_dev_bounded(const priskv_crc_ctx *ctx, const void *d_base, const uint64_t *d_offsets,
+                                    const uint32_t *d_lengths, uint64_t n, uint64_t max_len,
+                                    const uint32_t *d_expected, uint64_t *d_status, void *stream);
+
 /* Host-resident per-value extents -- the memfile scrub at recovery
  * (server/kv.c:824-875 walks the keys; each live value is valuelen bytes at
  * value_off inside the value region, server/memory.h:50-51).  The kernel

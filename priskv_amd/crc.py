@@ -51,6 +51,9 @@ SIGNATURES = [
      [_C.c_void_p, _C.c_void_p, _C.c_void_p, _C.c_void_p, _C.c_uint64, _C.c_uint64, _C.c_void_p, _C.c_void_p]),
     ("priskv_crc32_verify_dev", _C.c_int,
      [_C.c_void_p, _C.c_void_p, _C.c_void_p, _C.c_void_p, _C.c_uint64, _C.c_void_p, _C.c_void_p, _C.c_void_p]),
+    ("priskv_crc32_verify_dev_bounded", _C.c_int,
+     [_C.c_void_p, _C.c_void_p, _C.c_void_p, _C.c_void_p, _C.c_uint64, _C.c_uint64, _C.c_void_p, _C.c_void_p,
+      _C.c_void_p]),
     ("priskv_crc32_blocks_host", _C.c_int,
      [_C.c_void_p, _C.c_void_p, _C.c_uint64, _C.c_uint32, _C.c_void_p]),
     ("priskv_crc32_ranges_host", _C.c_int,
@@ -259,10 +262,11 @@ class CrcContext:
                "priskv_crc32_ranges_dev")
         return out
 
-    def verify_dev(self, region, offsets, lengths, expected, status=None, stream=None):
+    def verify_dev(self, region, offsets, lengths, expected, status=None, stream=None, max_len=None):
         """Device verify (priskv_crc32_verify_dev): returns the 2-entry int64
         status tensor {mismatches, first mismatching index or -1 (UINT64_MAX)},
-        filled asynchronously on `stream`."""
+        filled asynchronously on `stream`.  max_len: a host-known bound on the
+        lengths (priskv_crc32_verify_dev_bounded, a launch hint only)."""
         import torch
         n = offsets.numel()
         if (lengths.numel() != n or expected.numel() != n or offsets.dtype != torch.int64
@@ -273,6 +277,12 @@ class CrcContext:
         if status.numel() < 2 or status.element_size() != 8:
             raise ValueError("status must be an 8-byte tensor of >= 2 entries")
         _device_args(region, offsets, lengths, expected, status)
+        if max_len is not None:
+            _check(lib().priskv_crc32_verify_dev_bounded(self._h, region.data_ptr(), offsets.data_ptr(),
+                                                         lengths.data_ptr(), n, int(max_len), expected.data_ptr(),
+                                                         status.data_ptr(), _stream_ptr(stream)),
+                   "priskv_crc32_verify_dev_bounded")
+            return status
         _check(lib().priskv_crc32_verify_dev(self._h, region.data_ptr(), offsets.data_ptr(), lengths.data_ptr(),
                                              n, expected.data_ptr(), status.data_ptr(), _stream_ptr(stream)),
                "priskv_crc32_verify_dev")

@@ -2131,9 +2131,9 @@ int priskv_crc32_ranges_dev_bounded(const priskv_crc_ctx *ctx, const void *d_bas
                       max_len < 0xFFFFFFFFull ? max_len : 0xFFFFFFFFull);
 }
 
-int priskv_crc32_verify_dev(const priskv_crc_ctx *ctx, const void *d_base, const uint64_t *d_offsets,
-                            const uint32_t *d_lengths, uint64_t n, const uint32_t *d_expected,
-                            uint64_t *d_status, void *stream)
+namespace {
+int verify_dev(const priskv_crc_ctx *ctx, const void *d_base, const uint64_t *d_offsets, const uint32_t *d_lengths,
+               uint64_t n, const uint32_t *d_expected, uint64_t *d_status, void *stream, uint64_t max_len)
 {
     if (!ctx || !d_status)
         return -EINVAL;
@@ -2152,7 +2152,7 @@ int priskv_crc32_verify_dev(const priskv_crc_ctx *ctx, const void *d_base, const
     if (int rc = sc.get(n * sizeof(uint32_t)))
         return rc;
     uint32_t *got = static_cast<uint32_t *>(sc.p);
-    int rc = launch_extents(ctx, (const uint8_t *)d_base, n, d_offsets, d_lengths, 0, 0, got, s);
+    int rc = launch_extents(ctx, (const uint8_t *)d_base, n, d_offsets, d_lengths, 0, 0, got, s, max_len);
     if (!rc) {
         const uint64_t want = (n + 255) / 256;
         const uint32_t grid = (uint32_t)(want < (uint64_t)ctx->num_cus * 4 ? want : (uint64_t)ctx->num_cus * 4);
@@ -2160,6 +2160,23 @@ int priskv_crc32_verify_dev(const priskv_crc_ctx *ctx, const void *d_base, const
     }
     const int frc = sc.release();
     return rc ? rc : frc;
+}
+} // namespace
+
+int priskv_crc32_verify_dev(const priskv_crc_ctx *ctx, const void *d_base, const uint64_t *d_offsets,
+                            const uint32_t *d_lengths, uint64_t n, const uint32_t *d_expected,
+                            uint64_t *d_status, void *stream)
+{
+    return verify_dev(ctx, d_base, d_offsets, d_lengths, n, d_expected, d_status, stream, 0);
+}
+
+// max_len: a launch hint only, as priskv_crc32_ranges_dev_bounded's
+int priskv_crc32_verify_dev_bounded(const priskv_crc_ctx *ctx, const void *d_base, const uint64_t *d_offsets,
+                                    const uint32_t *d_lengths, uint64_t n, uint64_t max_len,
+                                    const uint32_t *d_expected, uint64_t *d_status, void *stream)
+{
+    return verify_dev(ctx, d_base, d_offsets, d_lengths, n, d_expected, d_status, stream,
+                      max_len < 0xFFFFFFFFull ? max_len : 0xFFFFFFFFull);
 }
 
 int priskv_crc_fill_splitmix_dev(const priskv_crc_ctx *ctx, void *d_dst, uint64_t nbytes, uint64_t seed,

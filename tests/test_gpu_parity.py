@@ -474,9 +474,20 @@ def test_verify_dev(torch_cuda, ctx):
     mism = np.nonzero(got != want)[0]
     st = ctx.verify_dev(t, d_o, d_l, d_e).cpu().tolist()
     assert st == [len(mism), int(mism[0])] and set(bad) <= set(mism.tolist())
+    # priskv_crc32_verify_dev_bounded: the same status with a tight, a wrong
+    # (too small) and an unknown bound, and on a few small values
+    for bound in (int(lens.max()), 100, 0):
+        assert ctx.verify_dev(t, d_o, d_l, d_e, max_len=bound).cpu().tolist() == st, bound
+    few = [i for i in bad if lens[i] <= 9000][:2] + [0, 1, 2]
+    sel = torch.tensor(few, dtype=torch.int64, device="cuda")
+    fst = ctx.verify_dev(t, d_o[sel], d_l[sel], d_e[sel], max_len=9000).cpu().tolist()
+    wrong = [j for j, i in enumerate(few) if i in set(mism.tolist())]
+    assert fst == [len(wrong), wrong[0] if wrong else -1]
     # empty batch
     e = torch.empty(0, dtype=torch.int64, device="cuda")
     st = ctx.verify_dev(t, e, e.to(torch.int32), e.to(torch.int32)).cpu().tolist()
+    assert st == [0, -1]
+    st = ctx.verify_dev(t, e, e.to(torch.int32), e.to(torch.int32), max_len=4096).cpu().tolist()
     assert st == [0, -1]
 
 
